@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: fused conditional-flow log_prob on MI355X.
+
+Metric (BASELINE.json): "log_prob evals/sec (whole node), 10-flow planar+radial
+chain, y_dim=1".  Default workload = config C2 per GPU: B = 2^24 samples,
+y_dim = 1, flows ("planar","radial") x 5, trainable base => P = 32 floats of
+per-sample parameters.  Multi-GPU (C4 form): every rank owns its own 2^24 batch
+(weak scaling) and the step ends with ONE RCCL all-reduce of (sum log_prob,
+count) — the mean log-likelihood.
+
+One step = the fused chain kernel over the rank's batch (writes log_prob (B,)
+and per-workgroup fp64 partial sums) + the partials reduce + (N > 1) the
+all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
+resident in HBM before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from normalizingflownetwork_amd import ops  # noqa: E402
+from normalizingflownetwork_amd.parallel import init_from_env  # noqa: E402
+
+C2_FLOWS = ("planar", "radial") * 5
+CONFIGS = {
+    # name: (flow_types, d, batch per GPU, draws or None)
+    "C2": (C2_FLOWS, 1, 1 << 24, None),
+    "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22, None),
+    "C5": (C2_FLOWS, 1, 1 << 17, 64),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes_per_launch(d: int, P: int, B: int, S) -> float:
+    """4*d (y) + 4*P (t) + 4 (log_prob) per eval; the posterior
+    reads t once per (draw, sample) and y / writes out once per sample."""
+    if S is None:
+        return float(B) * (4 * d + 4 * P + 4)
+    return float(B) * (S * 4 * P + 4 * d + 4)
+
+
+def cpu_baseline(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 20) -> dict:
+    """The reference-path stand-in timed on this host: the oracle's fp32 op-by-op
+    numpy restatement (whole-batch ops, TF-eager op order) on a bounded slice."""
+    from oracle import nfn_oracle as O
+
+    ft, d, _, S = CONFIGS[cfg]
+    rows = sample_rows if S is None else max(1, sample_rows // S)
+    P = O.total_param_size(ft, d, True)
+    rng = np.random.default_rng(22)
+    y = rng.standard_normal((rows, d)).astype(np.float32)
+    if S is None:
+        t = rng.standard_normal((rows, P)).astype(np.float32)
+        run = lambda: O.chain_log_prob(y, t, ft, d, True, np.float32)  # noqa: E731
+    else:
+        t = rng.standard_normal((S, rows, P)).astype(np.float32)
+        run = lambda: O.posterior_lse(y, t, ft, d, True, dtype=np.float32)  # noqa: E731
+    run()  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 50:
+            break
+    evals = reps * rows * (1 if S is None else S)
+    return {
+        "value": evals / el,
+        "unit": "evals/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{rows} samples{'' if S is None else f' x {S} draws'} of {cfg}, numpy fp32 op-by-op restatement "
+                  f"of the TF eager path (oracle/nfn_oracle.py), {reps} reps in {el:.1f}s, 1 thread",
+    }
+
+
+def load_traffic(cfg: str, B: int):
+    """Per-launch HBM bytes of the chain kernel from committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py -> profiles/*pmc_<cfg>.json), or None."""
+    import glob
+
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", f"*pmc_{cfg}.json")))
+    if not cands:
+        return None, None
+    with open(cands[-1]) as f:
+        rec = json.load(f)
+    if int(rec.get("batch", -1)) != B:
+        return None, None
+    return float(rec["hbm_bytes_per_launch"]), os.path.relpath(cands[-1], REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="override the per-GPU batch")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--math", default="fast", choices=["fast", "precise"])
+    args = ap.parse_args()
+
+    rank, world, local_rank = init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    ops.set_math_mode(args.math)
+
+    ft, d, B, S = CONFIGS[args.config]
+    if args.batch:
+        B = args.batch
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device=dev).manual_seed(22 + rank)
+    y = torch.randn((B, d), generator=gen, device=dev)
+    t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
+    launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    red = torch.zeros((2,), dtype=torch.float64, device=dev)
+    evals_per_step = B * (1 if S is None else S)
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        launcher.launch(sh)
+        if ev1 is not None:
+            ev1.record(stream)
+        s = launcher.finish_sum(sh)
+        if world > 1:
+            red[0:1].copy_(s)
+            red[1] = float(B)
+            dist.all_reduce(red)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        step(e0, e1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        kt = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kern_ms = float(kt.item())
+    mean_ll = float(red[0].item() / red[1].item()) if world > 1 else float(launcher.sum.item()) / B
+
+    if rank == 0:
+        total_evals = evals_per_step * world * args.steps
+        value = total_evals / elapsed
+        bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
+        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = load_traffic(args.config, B)
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.config, seconds=args.cpu_seconds)
+        wl = {
+            "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
+            "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
+            "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
+        }[args.config]
+        line = {
+            "metric": "log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"
+            if args.config == "C2" else f"log_prob evals/sec (whole node), {args.config}",
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic N(0,1) y and per-sample flow params t, generated on device (seed 22+rank)",
+            "config": {
+                "workload": wl,
+                "batch_per_gpu": B,
+                "global_batch": B * world,
+                "draws": S,
+                "y_dim": d,
+                "flows": list(ft),
+                "param_width": P,
+                "trainable_base": True,
+                "math": args.math,
+                "parallelism": f"dp{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "chain_logprob_kernel" if S is None else "posterior_lse_kernel",
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "traffic_source": traffic_src,
+            },
+            "cpu_baseline": cpu,
+            "mean_log_prob": mean_ll,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+/*
+ * nfn.h — C ABI of libnfn_hip.so, the MI355X (gfx950) implementation of the
+ * conditional normalizing-flow log_prob hot path of siboehm/NormalizingFlowNetwork.
+ *
+ * Conventions
+ *   - Every tensor pointer is DEVICE memory, caller-owned.  Nothing is allocated
+ *     inside a compute call; scratch is passed in (`workspace`).
+ *   - `flow_ids` is a HOST array (flow metadata, read while launching).
+ *   - Calls are stream-ordered on `stream` (a hipStream_t; NULL = default stream)
+ *     and return without synchronising.
+ *   - Return value: 0 = ok; < 0 = error (see NFN_E_*); the message of the last
+ *     error on the calling thread is returned by nfn_last_error().
+ *   - Flow ids: 0 = planar, 1 = radial, 2 = affine (the reference's FLOWS
+ *     registry, estimators/normalizing_flows/__init__.py:5).
+ *   - `flow_ids[0..K-1]` is APPLICATION order, i.e. the reference's
+ *     `flow_types` order.  The parameter row `t` is laid out exactly as the
+ *     reference's Dense output: [base (2d if trainable_base) | block of
+ *     flow_types[K-1] | ... | block of flow_types[0]]
+ *     (estimators/DistributionLayers.py:252, 270-277).
+ *   - Batch strides are in ELEMENTS (floats).  A stride of 0 broadcasts one row
+ *     over the batch (tests/test_flows.py:22-29 feeds y of batch 1 against
+ *     params of batch B).
+ *
+ * Reference interfaces replaced (file:line in the reference checkout):
+ *   nfn_chain_logprob_f32  <- InverseNormalizingFlowLayer._get_distribution_fn(...)(t)
+ *                             .log_prob(y)          estimators/DistributionLayers.py:245-255
+ *                             incl. _get_bijector    estimators/DistributionLayers.py:267-278
+ *                             and _get_base_dist     estimators/DistributionLayers.py:280-294;
+ *                             with y_mean/y_std it is BaseEstimator.log_pdf's
+ *                             "log_prob(y_circ) - sum(log y_std)"
+ *                                                    estimators/BaseEstimator.py:77-86
+ *                             and out_sum feeds score()/mle_log_likelihood_score
+ *                                                    estimators/BaseEstimator.py:43-47,
+ *                                                    evaluation/scorers.py:30-34
+ *   nfn_flow_fwd_ldj_f32   <- PlanarFlow._forward/_forward_log_det_jacobian
+ *                                                    estimators/normalizing_flows/PlanarFlow.py:20-80
+ *                             RadialFlow._forward/_forward_log_det_jacobian
+ *                                                    estimators/normalizing_flows/RadialFlow.py:20-84
+ *                             AffineFlow (tfp Affine) estimators/normalizing_flows/AffineFlow.py:4-9
+ *   nfn_posterior_lse_f32  <- BayesianNNEstimator.score per-sample logsumexp
+ *                                                    estimators/BayesianNNEstimator.py:65-76,
+ *                                                    evaluation/scorers.py:13-27
+ *   nfn_param_size /
+ *   nfn_total_param_size   <- Flow.get_param_size    PlanarFlow.py:35-41, RadialFlow.py:36-42,
+ *                                                    AffineFlow.py:11-17
+ *                             InverseNormalizingFlowLayer.get_total_param_size
+ *                                                    estimators/DistributionLayers.py:257-265
+ */
+#ifndef NFN_H_
+#define NFN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NFN_FLOW_PLANAR 0
+#define NFN_FLOW_RADIAL 1
+#define NFN_FLOW_AFFINE 2
+
+#define NFN_MAX_FLOWS 64
+#define NFN_MAX_DIMS 32
+
+#define NFN_OK 0
+#define NFN_E_SHAPE -1     /* bad batch / width / stride / dims            */
+#define NFN_E_FLOW_ID -2   /* unknown flow id or too many flows            */
+#define NFN_E_NULLPTR -3   /* required pointer is NULL                     */
+#define NFN_E_HIP -4       /* HIP runtime error (launch, no device, ...)   */
+
+/* Library version as MAJOR*10000 + MINOR*100 + PATCH. */
+int32_t nfn_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* nfn_last_error(void);
+
+/* Transcendental implementation used by later launches in this process:
+ * 0 = fast (gfx950 v_exp/v_log/v_rcp with stable rewrites; the default),
+ * 1 = precise (OCML expf/logf/log1pf/tanhf, IEEE division).
+ * The initial value comes from the environment variable NFN_MATH=fast|precise.
+ * Returns the previous mode, or NFN_E_SHAPE for an unknown mode. */
+int32_t nfn_set_math_mode(int32_t mode);
+
+/* Width of one flow's parameter block for event dimension d; < 0 on bad id. */
+int32_t nfn_param_size(int32_t flow_id, int32_t d);
+
+/* Total width P of a parameter row: sum of blocks + 2d if trainable_base. */
+int32_t nfn_total_param_size(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable_base);
+
+/* Number of doubles of device workspace nfn_chain_logprob_f32 needs when
+ * out_sum != NULL (per-workgroup partial sums). */
+int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
+
+/*
+ * Fused chain log-density.
+ *   out_logp[b] = log N(z_K; base(t_b)) + sum_k fldj_k(z_k; theta_k(t_b)) [- sum_j log y_std_j]
+ * with z_0 = y_b (or (y_b - y_mean)/y_std when y_mean/y_std are given).
+ *   y          : (B or 1, d) rows at y_bstride floats (0 = broadcast)
+ *   t          : (B or 1, P) rows at t_rowstride floats (0 = broadcast), P = nfn_total_param_size
+ *   y_mean/y_std : (d,) device arrays or both NULL
+ *   out_logp   : (B,) may be NULL when only the sum is wanted
+ *   out_sum    : device double[1] or NULL — receives sum_b out_logp[b] (fp64 accumulation)
+ *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
+ *                With out_sum == NULL and workspace != NULL only the per-workgroup
+ *                partial sums are written (finish with nfn_reduce_sum_f64).
+ */
+int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
+                              int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
+                              int32_t trainable_base, const float* y_mean, const float* y_std,
+                              float* out_logp, double* out_sum, double* workspace, void* stream);
+
+/*
+ * One bijector, forward direction: z_out = f(z), ldj_out = log|det df/dz| (B,).
+ *   z     : (B or 1, d) rows at z_bstride (0 = broadcast)
+ *   t_k   : (B or 1, nfn_param_size(flow_id, d)) rows at t_rowstride (0 = broadcast);
+ *           a column slice of a wider parameter row is passed as base pointer + stride
+ *   z_out : (B, d) contiguous, may be NULL; ldj_out : (B,), may be NULL
+ */
+int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
+                             int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out,
+                             void* stream);
+
+/* out[0] = sum of the n doubles at `in` (device), one workgroup, fixed order
+ * (deterministic).  Finishes a partials-only chain / posterior call. */
+int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream);
+
+/* Number of doubles of device workspace nfn_posterior_lse_f32 needs when out_sum != NULL. */
+int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P);
+
+/*
+ * Bayesian posterior score per sample:
+ *   out_lse[b] = logsumexp_s( logp(y_b | t[s, b]) [- sum log y_std] ) - log(S)
+ *   t : S draws; draw s, sample b at t + s*t_drawstride + b*t_rowstride
+ *   out_sum (nullable) receives sum_b out_lse[b] (fp64).
+ */
+int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
+                              int64_t t_rowstride, int32_t S, int64_t B, int32_t d,
+                              const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                              const float* y_mean, const float* y_std, float* out_lse, double* out_sum,
+                              double* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NFN_H_ */

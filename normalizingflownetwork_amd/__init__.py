@@ -1,0 +1,31 @@
+"""MI355X-native conditional normalizing-flow ``log_prob`` (drop-in for the flow
+path of siboehm/NormalizingFlowNetwork).
+
+Layout:
+  csrc/nfn_kernels.hip   HIP kernels for gfx950 + the extern "C" ABI (include/nfn.h)
+  _lib.py                ctypes binding of libnfn_hip.so (no CPU fallback)
+  ops.py                 torch-tensor entry points (device memory + stream plumbing)
+  normalizing_flows/     PlanarFlow / RadialFlow / AffineFlow, FLOWS, Chain, Invert
+  distribution_layers.py InverseNormalizingFlowLayer and its flow distribution
+  estimators.py          NormalizingFlowNetwork / BayesNormalizingFlowNetwork eval surface
+  scorers.py             mle / bayesian log-likelihood scorers
+  parallel.py            batch-sharded multi-GPU mean log-likelihood (RCCL all-reduce)
+"""
+
+from .distribution_layers import FlowDistribution, InverseNormalizingFlowLayer, TensorShape
+from .normalizing_flows import FLOWS, AffineFlow, Bijector, Chain, Invert, PlanarFlow, RadialFlow
+
+__version__ = "0.1.0"
+
+__all__ = [
+    "FLOWS",
+    "PlanarFlow",
+    "RadialFlow",
+    "AffineFlow",
+    "Bijector",
+    "Chain",
+    "Invert",
+    "InverseNormalizingFlowLayer",
+    "FlowDistribution",
+    "TensorShape",
+]

@@ -1,0 +1,90 @@
+"""ctypes binding of ``libnfn_hip.so`` (C ABI declared in ``include/nfn.h``).
+
+There is no CPU fallback: if the library is missing every compute entry point
+raises ``RuntimeError``.  The library is built in-tree by
+``python -m normalizingflownetwork_amd.build`` (or ``__graft_entry__.build()``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_NAME = "libnfn_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+# Symbols declared in include/nfn.h, with their ctypes signatures.
+_c_int32 = ctypes.c_int32
+_c_int64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+
+SIGNATURES = {
+    "nfn_version": (_c_int32, []),
+    "nfn_last_error": (ctypes.c_char_p, []),
+    "nfn_set_math_mode": (_c_int32, [_c_int32]),
+    "nfn_reduce_sum_f64": (_c_int32, [_vp, _c_int64, _vp, _vp]),
+    "nfn_param_size": (_c_int32, [_c_int32, _c_int32]),
+    "nfn_total_param_size": (_c_int32, [_vp, _c_int32, _c_int32, _c_int32]),
+    "nfn_chain_workspace_doubles": (_c_int64, [_c_int64, _c_int32, _c_int32]),
+    "nfn_posterior_workspace_doubles": (_c_int64, [_c_int64, _c_int32, _c_int32]),
+    "nfn_chain_logprob_f32": (
+        _c_int32,
+        [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp, _vp, _vp, _vp],
+    ),
+    "nfn_flow_fwd_ldj_f32": (
+        _c_int32,
+        [_c_int32, _vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _vp, _vp],
+    ),
+    "nfn_posterior_lse_f32": (
+        _c_int32,
+        [
+            _vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _c_int64, _c_int32, _vp, _c_int32, _c_int32,
+            _vp, _vp, _vp, _vp, _vp, _vp,
+        ],
+    ),
+}
+
+# Status codes (include/nfn.h)
+NFN_OK = 0
+NFN_E_SHAPE = -1
+NFN_E_FLOW_ID = -2
+NFN_E_NULLPTR = -3
+NFN_E_HIP = -4
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_NAME} is not built (expected at {LIB_PATH}); run "
+            "`python -m normalizingflownetwork_amd.build`. There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().nfn_last_error().decode("utf-8", "replace")
+
+
+def check(rc: int, what: str) -> None:
+    """Map a C-ABI status to the reference's exception types: shape / width /
+    flow-name problems are ``AssertionError`` (the reference asserts,
+    ``PlanarFlow.py:22``, ``DistributionLayers.py:231,272``); HIP failures are
+    ``RuntimeError``."""
+    if rc == NFN_OK:
+        return
+    msg = f"{what}: {last_error()} (status {rc})"
+    if rc in (NFN_E_SHAPE, NFN_E_FLOW_ID, NFN_E_NULLPTR):
+        raise AssertionError(msg)
+    raise RuntimeError(msg)

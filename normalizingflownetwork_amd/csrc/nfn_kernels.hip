@@ -1,0 +1,719 @@
+// nfn_kernels.hip — gfx950 (MI355X) kernels for the conditional normalizing-flow
+// log_prob hot path, and the extern "C" ABI declared in include/nfn.h.
+//
+// Reference semantics (paths in the reference checkout):
+//   PlanarFlow  estimators/normalizing_flows/PlanarFlow.py:20-80
+//   RadialFlow  estimators/normalizing_flows/RadialFlow.py:20-84
+//   AffineFlow  estimators/normalizing_flows/AffineFlow.py:4-17  (tfp Affine, diag scale)
+//   layer       estimators/DistributionLayers.py:245-294  (reversed param layout,
+//               Invert(Chain(...)), MultivariateNormalDiag base)
+//   estimator   estimators/BaseEstimator.py:77-86  (y normalisation, -sum(log y_std))
+//   posterior   estimators/BayesianNNEstimator.py:65-76, evaluation/scorers.py:13-27
+//
+// Design (DESIGN.md has the full story):
+//   * One workgroup owns a tile of `rows` consecutive samples (one sample per lane).
+//     The tile's parameter rows t[b0 .. b0+rows) are one contiguous HBM region;
+//     the workgroup streams it with coalesced 16-byte loads and writes it to LDS
+//     with an ODD row stride, so the per-lane parameter reads that follow
+//     (ds_read_b32 at a wave-uniform column offset) are bank-conflict free.
+//   * The flow chain is a runtime program (flow type + parameter offset per step,
+//     wave-uniform, read from the kernel arguments by scalar loads).  z and the
+//     running sum of log-det-Jacobians live in VGPRs for the whole chain; nothing
+//     but log_prob (and one fp64 partial sum per workgroup) is written back.
+//   * The event dimension is a template bound DM (1,2,4,8,16,32) with the runtime
+//     d <= DM guarding the unrolled loops, so z stays in registers.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+
+#include "nfn.h"
+
+#define NFN_VERSION_NUM 100  // 0.1.0
+
+namespace {
+
+constexpr int kMaxBlock = 256;
+constexpr int kLdsTileBudget = 48 * 1024;  // bytes of LDS per workgroup for the tile
+constexpr float kSoftplusThr = 13.942384719848633f;  // -(log(FLT_EPSILON) + 2), TF SoftplusOp
+constexpr float kLogExpm1One = 0.54132485461291810f; // log(expm1(1))
+constexpr float kHalfLog2Pi = 0.91893853320467274f;   // 0.5*log(2*pi)
+constexpr float kLn2 = 0.69314718055994531f;
+constexpr float kLog2e = 1.44269504088896341f;
+
+struct FlowProgram {
+  int32_t K;
+  int32_t step[NFN_MAX_FLOWS];  // (param offset << 2) | flow id, application order
+};
+
+struct ChainArgs {
+  const float* y;
+  const float* t;
+  const float* y_mean;
+  const float* y_std;
+  float* out;
+  double* partials;
+  int64_t y_bstride;
+  int64_t t_rowstride;
+  int64_t t_drawstride;
+  int64_t B;
+  int32_t d;
+  int32_t P;
+  int32_t lds_stride;  // odd, >= P
+  int32_t trainable;
+  int32_t S;           // posterior draws (1 for the plain chain)
+  int32_t vec4;        // tile rows can be streamed as float4
+  FlowProgram prog;
+};
+
+// ---------------------------------------------------------------------------
+// Math.  FAST uses the gfx950 transcendental unit directly (v_exp_f32, v_log_f32,
+// v_rcp_f32) with algebraic rewrites chosen to keep ABSOLUTE error ~1e-7 on every
+// quantity that is later added into log_prob; the precise path uses OCML.
+// ---------------------------------------------------------------------------
+
+template <bool FAST>
+__device__ __forceinline__ float f_exp(float x) {
+  if constexpr (FAST) {
+    return __builtin_amdgcn_exp2f(x * kLog2e);
+  } else {
+    return expf(x);
+  }
+}
+
+template <bool FAST>
+__device__ __forceinline__ float f_log(float x) {
+  if constexpr (FAST) {
+    return __builtin_amdgcn_logf(x) * kLn2;
+  } else {
+    return logf(x);
+  }
+}
+
+template <bool FAST>
+__device__ __forceinline__ float f_div(float a, float b) {
+  if constexpr (FAST) {
+    return a * __builtin_amdgcn_rcpf(b);
+  } else {
+    return a / b;
+  }
+}
+
+// log1p(e) for e >= 0.  FAST: log(u) * e / (u - 1) with u = 1 + e (exact for the
+// rounding of u, so relative accuracy is that of log).
+template <bool FAST>
+__device__ __forceinline__ float f_log1p_pos(float e) {
+  if constexpr (FAST) {
+    const float u = 1.0f + e;
+    const float den = u - 1.0f;
+    const float l = __builtin_amdgcn_logf(u) * kLn2;
+    return den == 0.0f ? e : l * (e * __builtin_amdgcn_rcpf(den));
+  } else {
+    return log1pf(e);
+  }
+}
+
+// tf.nn.softplus (TF SoftplusOp): x if x > 13.94, exp(x) if x < -13.94, else log1p(exp(x)).
+template <bool FAST>
+__device__ __forceinline__ float softplus_tf(float x) {
+  if constexpr (FAST) {
+    // max(x,0) + log1p(exp(-|x|)): same function, exp argument <= 0.
+    const float e = f_exp<true>(-fabsf(x));
+    const float sp = fmaxf(x, 0.0f) + f_log1p_pos<true>(e);
+    return x > kSoftplusThr ? x : sp;
+  } else {
+    if (x > kSoftplusThr) return x;
+    const float e = expf(x);
+    if (x < -kSoftplusThr) return e;
+    return log1pf(e);
+  }
+}
+
+template <bool FAST>
+__device__ __forceinline__ float f_tanh(float a) {
+  if constexpr (FAST) {
+    const float e = f_exp<true>(-2.0f * fabsf(a));
+    const float th = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return copysignf(th, a);
+  } else {
+    return tanhf(a);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Bijectors.  `p` points at the flow's parameter block (LDS in the chain kernels,
+// global memory in the single-flow kernel).  Each updates z in place (forward)
+// and returns forward_log_det_jacobian evaluated at the input z.
+// ---------------------------------------------------------------------------
+
+// PlanarFlow.py:23-33 (u, w = t+1, b), _u_circ :49-53, _wzb :59, _forward :72,
+// _forward_log_det_jacobian :78-80.
+template <int DM, bool FAST, typename PTR>
+__device__ __forceinline__ float planar_step(float (&z)[DM], PTR p, int d) {
+  float u[DM], w[DM];
+  float wtu = 0.0f, nw2 = 0.0f, wz = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      u[j] = p[j];
+      w[j] = p[d + j] + 1.0f;
+      wtu += w[j] * u[j];
+      nw2 += w[j] * w[j];
+      wz += w[j] * z[j];
+    }
+  }
+  const float b = p[2 * d];
+  const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
+  const float norm_w2 = nw2 + 1e-9f;
+  const float coef = m_wtu - wtu;
+  const float th = f_tanh<FAST>(wz + b);
+  const float dth = 1.0f - th * th;
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      const float uh = u[j] + coef * f_div<FAST>(w[j], norm_w2);
+      z[j] = z[j] + uh * th;
+      s += uh * (dth * w[j]);
+    }
+  }
+  return f_log<FAST>(fabsf(1.0f + s));
+}
+
+// RadialFlow.py:24-33 (alpha, beta constraints), _r :45 (L1 norm), _h :48,
+// _forward :54-56, _forward_log_det_jacobian :62-70 (der_h = RealDiv grad ((-1/y)/y)).
+template <int DM, bool FAST, typename PTR>
+__device__ __forceinline__ float radial_step(float (&z)[DM], PTR p, int d) {
+  const float alpha = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
+  const float beta = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
+  float r = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) r += fabsf(z[j] - p[2 + j]);
+  }
+  const float yv = alpha + r;
+  float h, der_h;
+  if constexpr (FAST) {
+    h = __builtin_amdgcn_rcpf(yv);
+    der_h = -h * h;
+  } else {
+    h = 1.0f / yv;
+    der_h = (-1.0f / yv) / yv;
+  }
+  const float ab = alpha * beta;
+  const float abh = ab * h;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) z[j] = z[j] + abh * (z[j] - p[2 + j]);
+  }
+  const float A = 1.0f + abh;
+  const float Bv = A + (ab * der_h) * r;
+  float Ap = 1.0f;  // (1 + ab*h) ** (d - 1)
+  for (int j = 1; j < d; ++j) Ap *= A;
+  return f_log<FAST>(Ap * Bv);
+}
+
+// tfp.bijectors.Affine(shift=t[:d], scale_diag=1+t[d:2d]) — AffineFlow.py:5-9.
+template <int DM, bool FAST, typename PTR>
+__device__ __forceinline__ float affine_step(float (&z)[DM], PTR p, int d) {
+  float ldj = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      const float sc = 1.0f + p[d + j];
+      z[j] = z[j] * sc + p[j];
+      ldj += f_log<FAST>(fabsf(sc));
+    }
+  }
+  return ldj;
+}
+
+template <int DM, bool FAST, typename PTR>
+__device__ __forceinline__ float flow_step(int id, float (&z)[DM], PTR p, int d) {
+  if (id == NFN_FLOW_PLANAR) return planar_step<DM, FAST>(z, p, d);
+  if (id == NFN_FLOW_RADIAL) return radial_step<DM, FAST>(z, p, d);
+  return affine_step<DM, FAST>(z, p, d);
+}
+
+// MultivariateNormalDiag(loc=t[:d], scale=1e-3+softplus(log(expm1(1))+0.1 t[d:2d]))
+// .log_prob(x) — DistributionLayers.py:281-294; N(0, I) when not trainable.
+template <int DM, bool FAST, typename PTR>
+__device__ __forceinline__ float base_log_prob(const float (&x)[DM], PTR p, int d, bool trainable) {
+  float sq = 0.0f, logdet = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      if (trainable) {
+        const float s = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * p[d + j]);
+        const float zz = f_div<FAST>(x[j] - p[j], s);
+        sq += zz * zz;
+        logdet += f_log<FAST>(s);
+      } else {
+        sq += x[j] * x[j];
+      }
+    }
+  }
+  return -0.5f * sq - (kHalfLog2Pi * (float)d + logdet);
+}
+
+// z_0 = y (or (y - mean)/std, BaseEstimator.py:85); returns -sum(log std) or 0.
+template <int DM, bool FAST>
+__device__ __forceinline__ float load_y(float (&z)[DM], const ChainArgs& a, int64_t b) {
+  const float* yr = a.y + b * a.y_bstride;
+  float corr = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < a.d) {
+      z[j] = yr[j];
+      if (a.y_mean) {
+        z[j] = f_div<FAST>(z[j] - a.y_mean[j], a.y_std[j]);
+        corr += f_log<FAST>(a.y_std[j]);
+      }
+    } else {
+      z[j] = 0.0f;
+    }
+  }
+  return corr;
+}
+
+// log_prob of one sample whose parameter row sits at `row` (LDS).
+template <int DM, bool FAST>
+__device__ __forceinline__ float eval_chain(float (&z)[DM], const float* row, const ChainArgs& a) {
+  float ildj = 0.0f;
+  const int d = a.d;
+  for (int k = 0; k < a.prog.K; ++k) {
+    const int st = a.prog.step[k];  // wave-uniform (kernel argument)
+    ildj = ildj + flow_step<DM, FAST>(st & 3, z, row + (st >> 2), d);
+  }
+  return base_log_prob<DM, FAST>(z, row, d, a.trainable != 0) + ildj;
+}
+
+// Stream `nr` parameter rows of width P (global row stride rs) into LDS rows of
+// stride S.  Coalesced: consecutive lanes take consecutive 16-byte (or 4-byte)
+// pieces of the contiguous row block.
+__device__ __forceinline__ void stage_rows(float* lds, const float* __restrict__ src, int64_t rs, int nr,
+                                           int P, int S, bool vec4) {
+  const int nth = blockDim.x;
+  const int tid = threadIdx.x;
+  if (vec4) {
+    const int q = P >> 2;
+    const int n = nr * q;
+    const int step_r = nth / q, step_c = nth - (nth / q) * q;
+    int r = tid / q, c = tid - (tid / q) * q;
+    for (int i = tid; i < n; i += nth) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)r * rs + 4 * c);
+      float* dst = lds + r * S + 4 * c;
+      dst[0] = v.x;
+      dst[1] = v.y;
+      dst[2] = v.z;
+      dst[3] = v.w;
+      r += step_r;
+      c += step_c;
+      if (c >= q) {
+        c -= q;
+        r += 1;
+      }
+    }
+  } else {
+    const int n = nr * P;
+    const int step_r = nth / P, step_c = nth - (nth / P) * P;
+    int r = tid / P, c = tid - (tid / P) * P;
+    for (int i = tid; i < n; i += nth) {
+      lds[r * S + c] = src[(int64_t)r * rs + c];
+      r += step_r;
+      c += step_c;
+      if (c >= P) {
+        c -= P;
+        r += 1;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) s += red[w];
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  const int rows = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * rows;
+  const int nr = (int)min((int64_t)rows, a.B - b0);
+  const bool tb = a.t_rowstride == 0;
+  if (a.P > 0) {
+    stage_rows(lds, a.t + (tb ? 0 : b0 * a.t_rowstride), a.t_rowstride, tb ? 1 : nr, a.P, a.lds_stride,
+               a.vec4 != 0);
+  }
+  __syncthreads();
+  float lp = 0.0f;
+  if (tid < nr) {
+    float z[DM];
+    const int64_t b = b0 + tid;
+    const float corr = load_y<DM, FAST>(z, a, b);
+    lp = eval_chain<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
+    if (a.out) a.out[b] = lp;
+  }
+  if (a.partials) {
+    const double s = block_sum(tid < nr ? (double)lp : 0.0, red);
+    if (tid == 0) a.partials[blockIdx.x] = s;
+  }
+}
+
+// Posterior: the same tile walk once per draw, with an online logsumexp over draws.
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  const int rows = blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * rows;
+  const int nr = (int)min((int64_t)rows, a.B - b0);
+  const bool tb = a.t_rowstride == 0;
+  float y0[DM];
+  float corr = 0.0f;
+  if (tid < nr) corr = load_y<DM, FAST>(y0, a, b0 + tid);
+  float m = -INFINITY, acc = 0.0f;
+  for (int s = 0; s < a.S; ++s) {
+    if (s > 0) __syncthreads();  // previous draw's tile fully consumed
+    if (a.P > 0) {
+      stage_rows(lds, a.t + (int64_t)s * a.t_drawstride + (tb ? 0 : b0 * a.t_rowstride), a.t_rowstride,
+                 tb ? 1 : nr, a.P, a.lds_stride, a.vec4 != 0);
+    }
+    __syncthreads();
+    if (tid < nr) {
+      float z[DM];
+#pragma unroll
+      for (int j = 0; j < DM; ++j) z[j] = y0[j];
+      const float lp = eval_chain<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
+      // online logsumexp (scorers.py:25 uses scipy.special.logsumexp over axis 0)
+      if (lp > m) {
+        acc = (m == -INFINITY ? 0.0f : acc * f_exp<FAST>(m - lp)) + 1.0f;
+        m = lp;
+      } else if (lp > -INFINITY) {
+        acc += f_exp<FAST>(lp - m);
+      } else if (lp != lp) {
+        m = lp;  // NaN propagates
+      }
+    }
+  }
+  float res = 0.0f;
+  if (tid < nr) {
+    res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(acc);
+    res = res - f_log<FAST>((float)a.S);
+    if (a.out) a.out[b0 + tid] = res;
+  }
+  if (a.partials) {
+    const double s = block_sum(tid < nr ? (double)res : 0.0, red);
+    if (tid == 0) a.partials[blockIdx.x] = s;
+  }
+}
+
+// Single bijector over a batch (the per-flow Bijector API).  Parameters are read
+// straight from global memory: this path serves the Python Bijector objects,
+// not the fused chain.
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock)
+    flow_fwd_ldj_kernel(int32_t flow_id, const float* __restrict__ z_in, int64_t z_bstride,
+                        const float* __restrict__ tk, int64_t t_rowstride, int64_t B, int32_t d,
+                        float* __restrict__ z_out, float* __restrict__ ldj_out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float z[DM];
+  const float* zr = z_in + b * z_bstride;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) z[j] = (j < d) ? zr[j] : 0.0f;
+  const float ldj = flow_step<DM, FAST>(flow_id, z, tk + b * t_rowstride, d);
+  if (z_out) {
+#pragma unroll
+    for (int j = 0; j < DM; ++j)
+      if (j < d) z_out[b * d + j] = z[j];
+  }
+  if (ldj_out) ldj_out[b] = ldj;
+}
+
+__global__ void __launch_bounds__(1024) reduce_f64_kernel(const double* __restrict__ in, int64_t n,
+                                                          double* __restrict__ out) {
+  __shared__ double red[1024 / 64];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += in[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int32_t param_size(int32_t id, int32_t d) {
+  switch (id) {
+    case NFN_FLOW_PLANAR: return 2 * d + 1;
+    case NFN_FLOW_RADIAL: return d + 2;
+    case NFN_FLOW_AFFINE: return 2 * d;
+    default: return -1;
+  }
+}
+
+int g_math_mode = [] {
+  const char* e = getenv("NFN_MATH");
+  return (e && strcmp(e, "precise") == 0) ? 1 : 0;
+}();
+
+bool use_fast_math() { return g_math_mode == 0; }
+
+// Validates the flow list and fills the program (parameter offsets of the
+// reversed layout, DistributionLayers.py:270-277).  Returns P or < 0.
+int32_t build_program(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable, FlowProgram* prog) {
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims must be in [1, " + std::to_string(NFN_MAX_DIMS) + "]");
+  if (K < 0 || K > NFN_MAX_FLOWS) return fail(NFN_E_FLOW_ID, "number of flows must be in [0, " + std::to_string(NFN_MAX_FLOWS) + "]");
+  if (K > 0 && !flow_ids) return fail(NFN_E_NULLPTR, "flow_ids is NULL");
+  int32_t off = trainable ? 2 * d : 0;
+  // blocks are laid out for flow_types[K-1], ..., flow_types[0]
+  for (int32_t k = K - 1; k >= 0; --k) {
+    const int32_t ps = param_size(flow_ids[k], d);
+    if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_ids[k]));
+    if (prog) prog->step[k] = (off << 2) | flow_ids[k];
+    off += ps;
+  }
+  if (prog) prog->K = K;
+  return off;
+}
+
+int dm_for(int d) {
+  if (d <= 1) return 1;
+  if (d <= 2) return 2;
+  if (d <= 4) return 4;
+  if (d <= 8) return 8;
+  if (d <= 16) return 16;
+  return 32;
+}
+
+struct TileGeom {
+  int rows;
+  int lds_stride;
+  size_t lds_bytes;
+};
+
+TileGeom tile_geom(int P) {
+  TileGeom g;
+  g.lds_stride = P | 1;  // odd stride: conflict-free per-lane ds_read_b32
+  const size_t row_bytes = (size_t)g.lds_stride * sizeof(float);
+  int rows = kMaxBlock;
+  while (rows > 64 && (size_t)rows * row_bytes > (size_t)kLdsTileBudget) rows -= 64;
+  g.rows = rows;
+  g.lds_bytes = P > 0 ? (size_t)rows * row_bytes : 0;
+  return g;
+}
+
+template <int DM, bool FAST>
+void launch_chain(const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool posterior) {
+  if (posterior)
+    hipLaunchKernelGGL((posterior_lse_kernel<DM, FAST>), grid, block, lds, s, a);
+  else
+    hipLaunchKernelGGL((chain_logprob_kernel<DM, FAST>), grid, block, lds, s, a);
+}
+
+template <bool FAST>
+void launch_chain_dm(int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool post) {
+  switch (dm) {
+    case 1: launch_chain<1, FAST>(a, grid, block, lds, s, post); break;
+    case 2: launch_chain<2, FAST>(a, grid, block, lds, s, post); break;
+    case 4: launch_chain<4, FAST>(a, grid, block, lds, s, post); break;
+    case 8: launch_chain<8, FAST>(a, grid, block, lds, s, post); break;
+    case 16: launch_chain<16, FAST>(a, grid, block, lds, s, post); break;
+    default: launch_chain<32, FAST>(a, grid, block, lds, s, post); break;
+  }
+}
+
+int32_t check_hip(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NFN_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return NFN_OK;
+}
+
+int64_t n_tiles(int64_t B, int P) { return (B + tile_geom(P).rows - 1) / tile_geom(P).rows; }
+
+int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride, int64_t t_rowstride,
+                  int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                  const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
+                  void* stream, bool posterior) {
+  g_last_error.clear();
+  ChainArgs a;
+  memset(&a, 0, sizeof(a));
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
+  if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
+  if (posterior && S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B == 0) {
+    if (out_sum) {
+      if (hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+    }
+    return NFN_OK;
+  }
+  if (!y) return fail(NFN_E_NULLPTR, "y is NULL");
+  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
+  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
+  if (!out && !workspace) return NFN_OK;
+  const TileGeom g = tile_geom(P);
+  a.y = y;
+  a.t = t;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.out = out;
+  a.partials = workspace;
+  a.y_bstride = y_bstride;
+  a.t_rowstride = t_rowstride;
+  a.t_drawstride = t_drawstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = g.lds_stride;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = posterior ? S : 1;
+  a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((t_drawstride & 3) == 0) &&
+           ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  const int64_t nblk = (B + g.rows - 1) / g.rows;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
+  const int dm = dm_for(d);
+  if (use_fast_math())
+    launch_chain_dm<true>(dm, a, grid, block, g.lds_bytes, s, posterior);
+  else
+    launch_chain_dm<false>(dm, a, grid, block, g.lds_bytes, s, posterior);
+  int32_t rc = check_hip(posterior ? "posterior_lse_kernel launch" : "chain_logprob_kernel launch");
+  if (rc != NFN_OK) return rc;
+  if (out_sum) {
+    hipLaunchKernelGGL(reduce_f64_kernel, dim3(1), dim3(1024), 0, s, (const double*)workspace, nblk, out_sum);
+    rc = check_hip("reduce_f64_kernel launch");
+  }
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t nfn_version(void) { return NFN_VERSION_NUM; }
+
+const char* nfn_last_error(void) { return g_last_error.c_str(); }
+
+int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream) {
+  g_last_error.clear();
+  if (n < 0) return fail(NFN_E_SHAPE, "n must be >= 0");
+  if (!out || (n > 0 && !in)) return fail(NFN_E_NULLPTR, "in or out is NULL");
+  hipLaunchKernelGGL(reduce_f64_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), in, n, out);
+  return check_hip("reduce_f64_kernel launch");
+}
+
+int32_t nfn_set_math_mode(int32_t mode) {
+  if (mode != 0 && mode != 1) return fail(NFN_E_SHAPE, "math mode must be 0 (fast) or 1 (precise)");
+  const int32_t prev = g_math_mode;
+  g_math_mode = mode;
+  return prev;
+}
+
+int32_t nfn_param_size(int32_t flow_id, int32_t d) {
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
+  const int32_t ps = param_size(flow_id, d);
+  return ps < 0 ? fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id)) : ps;
+}
+
+int32_t nfn_total_param_size(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable_base) {
+  return build_program(flow_ids, K, d, trainable_base ? 1 : 0, nullptr);
+}
+
+int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
+  (void)d;
+  if (B <= 0) return 0;
+  return n_tiles(B, P < 0 ? 0 : P);
+}
+
+int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
+  return nfn_chain_workspace_doubles(B, d, P);
+}
+
+int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B,
+                              int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                              const float* y_mean, const float* y_std, float* out_logp, double* out_sum,
+                              double* workspace, void* stream) {
+  return run_chain(y, y_bstride, t, 0, t_rowstride, 1, B, d, flow_ids, K, trainable_base, y_mean, y_std, out_logp,
+                   out_sum, workspace, stream, false);
+}
+
+int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
+                              int64_t t_rowstride, int32_t S, int64_t B, int32_t d, const int32_t* flow_ids,
+                              int32_t K, int32_t trainable_base, const float* y_mean, const float* y_std,
+                              float* out_lse, double* out_sum, double* workspace, void* stream) {
+  return run_chain(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, flow_ids, K, trainable_base, y_mean, y_std,
+                   out_lse, out_sum, workspace, stream, true);
+}
+
+int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
+                             int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, void* stream) {
+  g_last_error.clear();
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
+  const int32_t ps = param_size(flow_id, d);
+  if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id));
+  if (B < 0 || z_bstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
+  if (z_bstride != 0 && z_bstride < d) return fail(NFN_E_SHAPE, "z batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < ps) return fail(NFN_E_SHAPE, "t row stride < flow param size");
+  if (B == 0 || (!z_out && !ldj_out)) return NFN_OK;
+  if (!z || !t_k) return fail(NFN_E_NULLPTR, "z or t_k is NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  const dim3 grid((unsigned)nblk), block(kMaxBlock);
+#define NFN_LAUNCH_FLOW(DMV, FASTV)                                                                      \
+  hipLaunchKernelGGL((flow_fwd_ldj_kernel<DMV, FASTV>), grid, block, 0, s, flow_id, z, z_bstride, t_k, \
+                     t_rowstride, B, d, z_out, ldj_out)
+#define NFN_LAUNCH_FLOW_DM(FASTV)             \
+  switch (dm_for(d)) {                        \
+    case 1: NFN_LAUNCH_FLOW(1, FASTV); break;   \
+    case 2: NFN_LAUNCH_FLOW(2, FASTV); break;   \
+    case 4: NFN_LAUNCH_FLOW(4, FASTV); break;   \
+    case 8: NFN_LAUNCH_FLOW(8, FASTV); break;   \
+    case 16: NFN_LAUNCH_FLOW(16, FASTV); break; \
+    default: NFN_LAUNCH_FLOW(32, FASTV); break; \
+  }
+  if (use_fast_math()) {
+    NFN_LAUNCH_FLOW_DM(true)
+  } else {
+    NFN_LAUNCH_FLOW_DM(false)
+  }
+#undef NFN_LAUNCH_FLOW_DM
+#undef NFN_LAUNCH_FLOW
+  return check_hip("flow_fwd_ldj_kernel launch");
+}
+
+}  // extern "C"

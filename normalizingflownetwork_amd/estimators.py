@@ -1,0 +1,238 @@
+"""Estimator surface around the flow hot path.
+
+Mirrors ``estimators/BaseEstimator.py:43-86``, ``MaximumLikelihoodNNEstimator.py``,
+``NormalizingFlowNetwork.py`` and ``BayesNormalizingFlowNetwork.py`` /
+``BayesianNNEstimator.py:65-76`` for EVALUATION: ``log_pdf``, ``pdf``, ``score``.
+
+The x -> t network (the reference's Keras Dense stack) is not on the hot path
+(out of scope); it is a small torch MLP here, used only to
+produce ``t``.  Everything from ``t`` to the density / score runs in the fused
+HIP kernels: the y normalisation ``(y - mu)/sigma``, the whole flow chain, the
+base density, the ``-sum(log sigma)`` correction and (for ``score``) the fp64
+batch sum.  Training (``fit``) is out of scope for this round — the reference
+trains with Keras autodiff; the fused backward is the next row.
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+from .distribution_layers import InverseNormalizingFlowLayer
+
+_ACTIVATIONS = {
+    "tanh": torch.tanh,
+    "relu": torch.relu,
+    "linear": lambda v: v,
+    "sigmoid": torch.sigmoid,
+    "elu": torch.nn.functional.elu,
+}
+
+
+class _MLP:
+    """Dense stack x -> t (``MaximumLikelihoodNNEstimator.py:37-44``), Glorot-uniform
+    weights and zero biases like Keras' ``Dense`` defaults."""
+
+    def __init__(self, n_in: int, hidden_sizes: Sequence[int], n_out: int, activation: str, seed: int):
+        assert type(hidden_sizes) in (tuple, list)
+        assert activation in _ACTIVATIONS, f"unknown activation {activation!r}"
+        g = torch.Generator().manual_seed(seed)
+        sizes = [n_in] + list(hidden_sizes) + [n_out]
+        self.weights, self.biases = [], []
+        for a, b in zip(sizes[:-1], sizes[1:]):
+            lim = float(np.sqrt(6.0 / (a + b)))
+            self.weights.append((torch.rand((a, b), generator=g) * 2 - 1) * lim)
+            self.biases.append(torch.zeros((b,)))
+        self.activation = activation
+        self._device = None
+
+    def to(self, device):
+        if self._device != device:
+            self.weights = [w.to(device) for w in self.weights]
+            self.biases = [b.to(device) for b in self.biases]
+            self._device = device
+        return self
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        act = _ACTIVATIONS[self.activation]
+        h = x
+        n = len(self.weights)
+        for i, (w, b) in enumerate(zip(self.weights, self.biases)):
+            h = h @ w + b
+            if i < n - 1:
+                h = act(h)
+        return h
+
+
+class BaseEstimator:
+    """Evaluation half of ``estimators/BaseEstimator.py``."""
+
+    def __init__(self, dist_layer: InverseNormalizingFlowLayer, n_dims_x: Optional[int] = None,
+                 hidden_sizes=(16, 16), activation="relu", random_seed=22, noise_reg=("fixed_rate", 0.0)):
+        assert len(noise_reg) == 2
+        self.dist_layer = dist_layer
+        self.n_dims = dist_layer.n_dims
+        self.hidden_sizes = tuple(hidden_sizes)
+        self.activation = activation
+        self.random_seed = random_seed
+        self.noise_fn_type, self.noise_scale_factor = noise_reg
+        self.x_mean = self.x_std = None
+        self.y_mean = np.zeros((self.n_dims,), np.float32)
+        self.y_std = np.ones((self.n_dims,), np.float32)
+        self._mlp = None
+        if n_dims_x is not None:
+            self._build(n_dims_x)
+
+    # --- x -> t -----------------------------------------------------------------
+    def _build(self, n_dims_x: int):
+        self._mlp = _MLP(n_dims_x, self.hidden_sizes, self.dist_layer.get_total_param_size(), self.activation,
+                         self.random_seed)
+        if self.x_mean is None:
+            self.x_mean = np.zeros((n_dims_x,), np.float32)
+            self.x_std = np.ones((n_dims_x,), np.float32)
+
+    def _assign_data_normalization(self, x, y):
+        """``BaseEstimator.py:49-53``."""
+        x = np.asarray(x, np.float32)
+        y = np.asarray(y, np.float32)
+        self.x_mean = np.mean(x, axis=0, dtype=np.float32)
+        self.y_mean = np.mean(y, axis=0, dtype=np.float32)
+        self.x_std = np.std(x, axis=0, dtype=np.float32)
+        self.y_std = np.std(y, axis=0, dtype=np.float32)
+
+    def set_data_normalization(self, x, y):
+        self._assign_data_normalization(x, y)
+
+    def params(self, x) -> torch.Tensor:
+        """``t = MLP((x - mu_x)/(sigma_x + 1e-8))`` (``MaximumLikelihoodNNEstimator.py:40-43``)."""
+        x = ops.as_device_f32(x)
+        if x.dim() == 1:
+            x = x.unsqueeze(-1)
+        if self._mlp is None:
+            self._build(int(x.shape[-1]))
+        dev = x.device
+        self._mlp.to(dev)
+        xm = torch.as_tensor(self.x_mean, device=dev)
+        xs = torch.as_tensor(self.x_std, device=dev)
+        return self._mlp((x - xm) / (xs + 1e-8)).contiguous()
+
+    def __call__(self, x):
+        return self.dist_layer(self.params(x))
+
+    def call(self, x, training=False):
+        return self(x)
+
+    # --- evaluation ---------------------------------------------------------------
+    def log_pdf(self, x, y):
+        """``BaseEstimator.py:77-86``: ``log_prob((y-mu)/sigma) - sum(log sigma)``."""
+        x = np.asarray(x, np.float32) if not isinstance(x, torch.Tensor) else x
+        y = np.asarray(y, np.float32) if not isinstance(y, torch.Tensor) else y
+        assert tuple(x.shape) == tuple(y.shape)
+        output = self(x)
+        assert output.event_shape == y.shape[-1]
+        return output.log_prob(y, self.y_mean, self.y_std)
+
+    def pdf(self, x, y):
+        """``BaseEstimator.py:71-75``: ``prob(y_circ) / prod(sigma)`` = ``exp(log_pdf)``."""
+        return torch.exp(self.log_pdf(x, y))
+
+    def score(self, x_data, y_data) -> float:
+        """``BaseEstimator.py:43-47``: mean log-likelihood, reduced on the device in fp64."""
+        x_data = np.asarray(x_data, np.float32) if not isinstance(x_data, torch.Tensor) else x_data
+        y_data = np.asarray(y_data, np.float32) if not isinstance(y_data, torch.Tensor) else y_data
+        output = self(x_data)
+        s = output.log_prob_sum(y_data, self.y_mean, self.y_std)
+        return float(s.item()) / int(y_data.shape[0])
+
+    def fit(self, *args, **kwargs):
+        raise NotImplementedError(
+            "training is out of scope for the log_prob hot path (SURVEY.md §2); the fused backward is next (§8(f))"
+        )
+
+
+class NormalizingFlowNetwork(BaseEstimator):
+    """``estimators/NormalizingFlowNetwork.py:9-19``: ``n_flows`` radial flows by
+    default.  ``flow_types`` (a compatible superset) picks any chain, e.g. the
+    planar/radial chains of the benchmark configs."""
+
+    def __init__(self, n_dims, n_flows=10, trainable_base_dist=True, flow_types=None, hidden_sizes=(16, 16),
+                 noise_reg=("fixed_rate", 0.0), learning_rate=3e-3, activation="relu", random_seed=22,
+                 n_dims_x=None):
+        flow_types = tuple(flow_types) if flow_types is not None else ("radial",) * n_flows
+        dist_layer = InverseNormalizingFlowLayer(flow_types=flow_types, n_dims=n_dims,
+                                                 trainable_base_dist=trainable_base_dist)
+        self.learning_rate = learning_rate
+        super().__init__(dist_layer, n_dims_x=n_dims_x, hidden_sizes=hidden_sizes, activation=activation,
+                         random_seed=random_seed, noise_reg=noise_reg)
+
+    @staticmethod
+    def build_function(n_dims=1, n_flows=3, hidden_sizes=(16, 16), trainable_base_dist=True,
+                       noise_reg=("fixed_rate", 0.0), learning_rate=3e-3, activation="tanh"):
+        return NormalizingFlowNetwork(n_dims=n_dims, n_flows=n_flows, hidden_sizes=hidden_sizes,
+                                      trainable_base_dist=trainable_base_dist, noise_reg=noise_reg,
+                                      learning_rate=learning_rate, activation=activation)
+
+
+class BayesNormalizingFlowNetwork(BaseEstimator):
+    """Posterior-scoring half of ``estimators/BayesNormalizingFlowNetwork.py`` /
+    ``BayesianNNEstimator.py``.  The weight posterior is mean-field Gaussian
+    (``BayesianNNEstimator.py:92-107``); each posterior draw re-samples the MLP
+    weights and yields a ``t`` draw.  ``score`` stacks the S draws as
+    ``t (S, B, P)`` and evaluates ``logsumexp_s(log_pdf) - log S`` per sample in
+    ONE fused kernel (``nfn_posterior_lse_f32``) instead of S model re-runs."""
+
+    def __init__(self, n_dims, kl_weight_scale=1.0, n_flows=2, trainable_base_dist=True, flow_types=None,
+                 hidden_sizes=(10,), activation="tanh", noise_reg=("fixed_rate", 0.0), learning_rate=2e-2,
+                 map_mode=False, prior_scale=1.0, posterior_scale=0.05, random_seed=22, n_dims_x=None):
+        assert kl_weight_scale <= 1.0  # BayesianNNEstimator.py:120
+        flow_types = tuple(flow_types) if flow_types is not None else ("radial",) * n_flows
+        dist_layer = InverseNormalizingFlowLayer(flow_types=flow_types, n_dims=n_dims,
+                                                 trainable_base_dist=trainable_base_dist)
+        self.map_mode = map_mode
+        self.prior_scale = prior_scale
+        self.posterior_scale = posterior_scale
+        self.kl_weight_scale = kl_weight_scale
+        super().__init__(dist_layer, n_dims_x=n_dims_x, hidden_sizes=hidden_sizes, activation=activation,
+                         random_seed=random_seed, noise_reg=noise_reg)
+        self._draw_gen = None
+
+    def params_draws(self, x, n_draws: int) -> torch.Tensor:
+        """``t`` for ``n_draws`` posterior weight samples: (S, B, P)."""
+        x = ops.as_device_f32(x)
+        if x.dim() == 1:
+            x = x.unsqueeze(-1)
+        if self._mlp is None:
+            self._build(int(x.shape[-1]))
+        dev = x.device
+        self._mlp.to(dev)
+        if self._draw_gen is None:
+            self._draw_gen = torch.Generator(device=dev).manual_seed(self.random_seed)
+        xm = torch.as_tensor(self.x_mean, device=dev)
+        xs = torch.as_tensor(self.x_std, device=dev)
+        xn = (x - xm) / (xs + 1e-8)
+        act = _ACTIVATIONS[self.activation]
+        draws = []
+        for _ in range(n_draws):
+            h = xn
+            n = len(self._mlp.weights)
+            for i, (w, b) in enumerate(zip(self._mlp.weights, self._mlp.biases)):
+                if not self.map_mode:
+                    w = w + self.posterior_scale * torch.randn(w.shape, generator=self._draw_gen, device=dev)
+                    b = b + self.posterior_scale * torch.randn(b.shape, generator=self._draw_gen, device=dev)
+                h = h @ w + b
+                if i < n - 1:
+                    h = act(h)
+            draws.append(h)
+        return torch.stack(draws).contiguous()
+
+    def score(self, x_data, y_data, n_draws: Optional[int] = None) -> float:
+        """``BayesianNNEstimator.py:65-76``: 50 draws (1 in map mode)."""
+        S = n_draws if n_draws is not None else (1 if self.map_mode else 50)
+        t = self.params_draws(np.asarray(x_data, np.float32), S)
+        _, s = ops.posterior_lse(np.asarray(y_data, np.float32), t, self.dist_layer.flow_types, self.n_dims,
+                                 self.dist_layer.trainable_base_dist, self.y_mean, self.y_std,
+                                 want_values=False, want_sum=True)
+        return float(s.item()) / int(np.shape(y_data)[0])

@@ -1,0 +1,259 @@
+"""Device-side entry points: torch device tensors in, HIP kernels via the C ABI.
+
+Every function here launches a kernel from ``libnfn_hip.so`` on torch's
+current HIP stream; torch provides only device memory and the stream handle.
+There is no CPU fallback — without a GPU these raise ``RuntimeError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+FLOW_IDS = {"planar": 0, "radial": 1, "affine": 2}
+
+_workspaces: dict = {}
+
+
+def _device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("normalizingflownetwork_amd needs a HIP device (MI355X); none is visible")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def as_device_f32(x, device: Optional[torch.device] = None) -> torch.Tensor:
+    """Convert array-likes / tensors to a float32 device tensor whose last dim is contiguous."""
+    dev = device or _device()
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=dev, dtype=torch.float32)
+    else:
+        t = torch.as_tensor(np.asarray(x, dtype=np.float32), device=dev)
+    if t.dim() >= 1 and t.shape[-1] > 1 and t.stride(-1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def _row_stride(x: torch.Tensor) -> int:
+    """Batch stride in elements of a (N, W) tensor; 0 broadcasts a single row."""
+    return 0 if x.shape[0] == 1 else int(x.stride(0))
+
+
+def _stream() -> int:
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(x: Optional[torch.Tensor]) -> Optional[int]:
+    return None if x is None else int(x.data_ptr())
+
+
+def flow_ids(flow_types: Sequence[str]):
+    for f in flow_types:
+        assert f in FLOW_IDS, f"unknown flow type {f!r}"  # DistributionLayers.py:231
+    ids = (ctypes.c_int32 * max(1, len(flow_types)))(*[FLOW_IDS[f] for f in flow_types])
+    return ids, len(flow_types)
+
+
+def param_size(flow_type: str, n_dims: int) -> int:
+    """Host metadata, same as the C ABI's ``nfn_param_size``: ``PlanarFlow.py:35-41`` (2d+1),
+    ``RadialFlow.py:36-42`` (d+2), ``AffineFlow.py:11-17`` (2d)."""
+    assert flow_type in FLOW_IDS, f"unknown flow type {flow_type!r}"
+    return {"planar": 2 * n_dims + 1, "radial": n_dims + 2, "affine": 2 * n_dims}[flow_type]
+
+
+def total_param_size(flow_types: Sequence[str], n_dims: int, trainable_base: bool) -> int:
+    """``InverseNormalizingFlowLayer.get_total_param_size`` (``DistributionLayers.py:257-265``)."""
+    return sum(param_size(f, n_dims) for f in flow_types) + (2 * n_dims if trainable_base else 0)
+
+
+def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
+    key = (device.type, device.index)
+    ws = _workspaces.get(key)
+    if ws is None or ws.numel() < n_doubles:
+        ws = torch.empty(max(1, n_doubles), dtype=torch.float64, device=device)
+        _workspaces[key] = ws
+    return ws
+
+
+def _prep_2d(x, width: int, name: str, device) -> torch.Tensor:
+    x = as_device_f32(x, device)
+    if x.dim() == 1:
+        x = x.unsqueeze(0)
+    assert x.dim() == 2, f"{name} must be 2-D (batch, {width}), got shape {tuple(x.shape)}"
+    assert x.shape[-1] == width, f"{name} last dimension must be {width}, got {x.shape[-1]}"
+    return x
+
+
+def chain_log_prob(
+    y,
+    t,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+    want_values: bool = True,
+    want_sum: bool = False,
+) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """Fused ``log_prob(y | t)`` over the whole flow chain (one kernel launch).
+
+    Returns ``(log_prob (B,) float32 | None, sum (1,) float64 | None)``.
+    With ``y_mean``/``y_std`` it is ``BaseEstimator.log_pdf``'s
+    ``log_prob((y-mu)/sigma) - sum(log sigma)`` (``BaseEstimator.py:77-86``).
+    """
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    y = _prep_2d(y, n_dims, "y", dev)
+    t = _prep_2d(t, P, "t", dev) if P > 0 else torch.zeros((1, 1), dtype=torch.float32, device=dev)
+    B = max(y.shape[0], t.shape[0] if P > 0 else 1)
+    assert y.shape[0] in (1, B) and (P == 0 or t.shape[0] in (1, B)), "incompatible batch sizes"
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+        assert ym.numel() == n_dims and ys.numel() == n_dims
+    out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
+    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    lib = _lib.load()
+    ws = _workspace(int(lib.nfn_chain_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
+    ids, k = flow_ids(flow_types)
+    rc = lib.nfn_chain_logprob_f32(
+        _ptr(y), _row_stride(y), _ptr(t), _row_stride(t) if P > 0 else 0, B, int(n_dims),
+        ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys),
+        _ptr(out), _ptr(osum), _ptr(ws), _stream(),
+    )
+    _lib.check(rc, "nfn_chain_logprob_f32")
+    return out, osum
+
+
+def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, want_ldj: bool = True):
+    """One bijector: ``(forward(z), forward_log_det_jacobian(z))`` (either may be None)."""
+    dev = _device()
+    ps = param_size(flow_type, n_dims)
+    z = _prep_2d(z, n_dims, "z", dev)
+    t_k = as_device_f32(t_k, dev)
+    if t_k.dim() == 1:
+        t_k = t_k.unsqueeze(0)
+    assert t_k.shape[-1] == ps, f"{flow_type} flow needs {ps} params, got {t_k.shape[-1]}"
+    B = max(z.shape[0], t_k.shape[0])
+    assert z.shape[0] in (1, B) and t_k.shape[0] in (1, B), "incompatible batch sizes"
+    z_out = torch.empty((B, n_dims), dtype=torch.float32, device=dev) if want_z else None
+    ldj = torch.empty((B,), dtype=torch.float32, device=dev) if want_ldj else None
+    lib = _lib.load()
+    rc = lib.nfn_flow_fwd_ldj_f32(
+        FLOW_IDS[flow_type], _ptr(z), _row_stride(z), _ptr(t_k), _row_stride(t_k), B, int(n_dims),
+        _ptr(z_out), _ptr(ldj), _stream(),
+    )
+    _lib.check(rc, "nfn_flow_fwd_ldj_f32")
+    return z_out, ldj
+
+
+def posterior_lse(
+    y,
+    t_draws,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+    want_values: bool = True,
+    want_sum: bool = False,
+):
+    """``logsumexp_s(log_pdf(y_b | t[s, b])) - log S`` per sample (``BayesianNNEstimator.py:65-76``).
+
+    ``t_draws``: (S, B, P) device tensor (rows contiguous)."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    y = _prep_2d(y, n_dims, "y", dev)
+    t_draws = as_device_f32(t_draws, dev)
+    assert t_draws.dim() == 3 and t_draws.shape[-1] == P, f"t_draws must be (S, B, {P})"
+    S, Bt = int(t_draws.shape[0]), int(t_draws.shape[1])
+    B = max(y.shape[0], Bt)
+    assert y.shape[0] in (1, B) and Bt in (1, B)
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
+    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    lib = _lib.load()
+    ws = _workspace(int(lib.nfn_posterior_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
+    ids, k = flow_ids(flow_types)
+    rc = lib.nfn_posterior_lse_f32(
+        _ptr(y), _row_stride(y), _ptr(t_draws), int(t_draws.stride(0)), 0 if Bt == 1 else int(t_draws.stride(1)),
+        S, B, int(n_dims), ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys),
+        _ptr(out), _ptr(osum), _ptr(ws), _stream(),
+    )
+    _lib.check(rc, "nfn_posterior_lse_f32")
+    return out, osum
+
+
+def set_math_mode(mode: str) -> str:
+    """Select the kernels' transcendental implementation for later launches:
+    ``"fast"`` (default) or ``"precise"``.  Returns the previous mode."""
+    assert mode in ("fast", "precise")
+    prev = _lib.load().nfn_set_math_mode(1 if mode == "precise" else 0)
+    _lib.check(prev if prev < 0 else 0, "nfn_set_math_mode")
+    return "precise" if prev == 1 else "fast"
+
+
+class ChainLauncher:
+    """Pre-bound fused-chain launch for repeated evaluation of fixed device
+    buffers (the benchmark / serving loop): all validation and pointer
+    marshalling happens once; ``launch()`` is a single C-ABI call.
+
+    ``launch()`` writes ``out`` (B,) and the per-workgroup fp64 partial sums;
+    ``finish_sum()`` reduces the partials into ``sum`` (1,) fp64."""
+
+    def __init__(self, y: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
+                 trainable_base: bool, write_values: bool = True, draws: Optional[int] = None):
+        self.lib = _lib.load()
+        dev = y.device
+        self.n_dims = int(n_dims)
+        self.P = total_param_size(flow_types, n_dims, trainable_base)
+        self.posterior = draws is not None
+        assert y.dim() == 2 and y.shape[1] == n_dims and y.stride(1) == 1
+        if self.posterior:
+            assert t.dim() == 3 and t.shape[0] == draws and t.shape[2] == self.P and t.stride(2) == 1
+            self.B = max(int(y.shape[0]), int(t.shape[1]))
+        else:
+            assert t.dim() == 2 and t.shape[1] == self.P and t.stride(1) == 1
+            self.B = max(int(y.shape[0]), int(t.shape[0]))
+        self.y, self.t = y, t
+        self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
+        self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
+        fn_ws = self.lib.nfn_posterior_workspace_doubles if self.posterior else self.lib.nfn_chain_workspace_doubles
+        self.n_partials = int(fn_ws(self.B, self.n_dims, self.P))
+        self.partials = torch.empty((max(1, self.n_partials),), dtype=torch.float64, device=dev)
+        self._ids, self._k = flow_ids(flow_types)
+        self._ids_p = ctypes.cast(self._ids, ctypes.c_void_p)
+        self._trainable = int(bool(trainable_base))
+        if self.posterior:
+            self._args = (
+                _ptr(y), _row_stride(y), _ptr(t), int(t.stride(0)), 0 if t.shape[1] == 1 else int(t.stride(1)),
+                int(draws), self.B, self.n_dims, self._ids_p, self._k, self._trainable, None, None,
+                _ptr(self.out), None, _ptr(self.partials),
+            )
+            self._fn = self.lib.nfn_posterior_lse_f32
+        else:
+            self._args = (
+                _ptr(y), _row_stride(y), _ptr(t), _row_stride(t), self.B, self.n_dims, self._ids_p, self._k,
+                self._trainable, None, None, _ptr(self.out), None, _ptr(self.partials),
+            )
+            self._fn = self.lib.nfn_chain_logprob_f32
+        self._sum_args = (_ptr(self.partials), self.n_partials, _ptr(self.sum))
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self._fn(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "fused chain launch")
+
+    def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
+        rc = self.lib.nfn_reduce_sum_f64(*self._sum_args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_reduce_sum_f64")
+        return self.sum

@@ -1,0 +1,356 @@
+"""CPU oracle for the conditional normalizing-flow ``log_prob`` hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product package
+(``normalizingflownetwork_amd``) imports this module.  It may be imported only by
+``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py``, and there only as the checker / the timed CPU stand-in, never as
+the thing measured or shipped.
+
+What it restates (all paths relative to the reference checkout):
+
+* ``estimators/normalizing_flows/PlanarFlow.py:20-80``   (planar bijector)
+* ``estimators/normalizing_flows/RadialFlow.py:20-84``   (radial bijector)
+* ``estimators/normalizing_flows/AffineFlow.py:4-17``    (TFP ``Affine`` with
+  ``shift=t[:d]``, ``scale_diag=1+t[d:2d]``)
+* ``estimators/DistributionLayers.py:245-294``           (param split in
+  REVERSED flow order, ``Invert(Chain(...))``, base ``MultivariateNormalDiag``)
+* ``estimators/BaseEstimator.py:43-86``                  (y normalisation and
+  the ``-sum(log y_std)`` correction of ``log_pdf`` / ``score``)
+* ``estimators/BayesianNNEstimator.py:65-76`` and
+  ``evaluation/scorers.py:13-34``                        (posterior logsumexp
+  score, MLE score)
+
+plus the semantics of the external, un-vendored TF/TFP pieces the reference
+drives (TF 2.0-2.3 / TFP 0.8-0.11 era, unpinned in ``requirements.txt:3-4``):
+
+* ``tf.nn.softplus`` (TF ``SoftplusOp``): ``x`` if ``x > -thr``, ``exp(x)`` if
+  ``x < thr``, else ``log1p(exp(x))``, ``thr = log(eps) + 2``;
+* ``tfp.bijectors.Chain([b0..bn]).forward(x) = b0(b1(...bn(x)))`` and its
+  ``forward_log_det_jacobian`` accumulates ``fldj`` in the same application
+  order; ``Invert(chain).inverse == chain.forward`` and
+  ``Invert(chain).inverse_log_det_jacobian == chain.forward_log_det_jacobian``;
+* ``TransformedDistribution.log_prob(y) = base.log_prob(x) + ildj(y)``;
+* ``MultivariateNormalDiag.log_prob(x) = -0.5*sum(z^2) - (0.5*d*log(2pi) +
+  sum(log|s|))`` with ``z = (x-loc)/s``;
+* the ``GradientTape`` derivative of ``h = 1/(alpha+r)`` used by
+  ``RadialFlow._forward_log_det_jacobian`` (``RadialFlow.py:63-66``) is TF's
+  ``RealDiv`` gradient ``((-1/y)/y)``.
+
+Two precisions:
+
+* ``np.float64`` — the mathematical truth used for parity.
+* ``np.float32`` — an op-by-op fp32 mirror of TF eager's evaluation order (each
+  TF op rounds to fp32).  Its deviation from the fp64 truth estimates the
+  reference's own fp32 error on a sample; the parity tolerance uses it for
+  ill-conditioned samples (see ``tolerance_bound``).  The same fp32 mirror,
+  run as whole-batch numpy ops, is the timed CPU stand-in for the reference's
+  TF eager CPU path (TF/TFP are not installed anywhere this runs).
+
+Parity pin status: the reference's own tests hold NO numeric log_prob values
+(``tests/test_flows.py`` checks shapes and symmetry only), and TF/TFP cannot be
+imported here, so numeric parity against TF itself is *unpinned*.  This oracle
+is pinned instead by (a) the reference tests' shape/size/order/symmetry
+properties, (b) analytic known-answer cases and (c) an independent torch-fp64
+autodiff Jacobian of every bijector (``tests/test_oracle.py``).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Sequence
+
+import numpy as np
+
+# ---------------------------------------------------------------------------
+# Registry metadata (``estimators/normalizing_flows/__init__.py:5``)
+# ---------------------------------------------------------------------------
+
+FLOW_IDS = {"planar": 0, "radial": 1, "affine": 2}
+
+
+def param_size(flow_type: str, d: int) -> int:
+    """``PlanarFlow.py:35-41`` (2d+1), ``RadialFlow.py:36-42`` (d+2),
+    ``AffineFlow.py:11-17`` (2d)."""
+    if flow_type == "planar":
+        return 2 * d + 1
+    if flow_type == "radial":
+        return d + 2
+    if flow_type == "affine":
+        return 2 * d
+    raise AssertionError(f"unknown flow type {flow_type!r}")
+
+
+def total_param_size(flow_types: Sequence[str], d: int, trainable_base: bool) -> int:
+    """``DistributionLayers.py:257-265``."""
+    return sum(param_size(f, d) for f in flow_types) + (2 * d if trainable_base else 0)
+
+
+def split_params(t: np.ndarray, flow_types: Sequence[str], d: int, trainable_base: bool):
+    """Return ``(base_block, [block_k for k in application order])``.
+
+    ``DistributionLayers.py:252``: the base takes ``t[..., :2d]`` when trainable;
+    ``DistributionLayers.py:270-277``: the flow blocks follow in REVERSED
+    ``flow_types`` order.  The list returned here is re-ordered to application
+    order (``flow_types[0]`` first), because ``Chain(reversed)`` applies
+    ``flow_types[0]`` first (pinned by ``tests/test_distribution_layers.py:234-242``).
+    """
+    o = 2 * d if trainable_base else 0
+    base = t[..., :o] if trainable_base else None
+    rest = t[..., o:]
+    rev = list(reversed(list(flow_types)))
+    sizes = [param_size(f, d) for f in rev]
+    assert sum(sizes) == rest.shape[-1], "param width mismatch"  # DistributionLayers.py:272
+    blocks_rev = []
+    begin = 0
+    for s in sizes:
+        blocks_rev.append(rest[..., begin : begin + s])
+        begin += s
+    return base, list(reversed(blocks_rev))
+
+
+# ---------------------------------------------------------------------------
+# Elementwise helpers (fp32 mirror keeps every intermediate in ``dt``)
+# ---------------------------------------------------------------------------
+
+
+def _c(x, dt):
+    return np.asarray(x, dtype=dt)
+
+
+def softplus(x: np.ndarray) -> np.ndarray:
+    """TF ``SoftplusOp`` (``tensorflow/core/kernels/softplus_op.h``)."""
+    dt = x.dtype
+    thr = dt.type(np.log(np.finfo(dt).eps) + 2.0)
+    with np.errstate(over="ignore"):
+        e = np.exp(x)
+        mid = np.log1p(e)
+    out = np.where(x > -thr, x, np.where(x < thr, e, mid))
+    return out.astype(dt, copy=False)
+
+
+def _log_expm1_one(dt):
+    # tf.math.log(tf.math.expm1(1.0)) evaluated in dtype dt
+    return dt.type(np.log(np.expm1(dt.type(1.0))))
+
+
+# ---------------------------------------------------------------------------
+# Bijectors.  z: (B, d); params: (B, p) or (1, p); every op rounds to dt.
+# ---------------------------------------------------------------------------
+
+
+def planar_params(tk: np.ndarray, d: int):
+    """``PlanarFlow.__init__`` + ``_u_circ`` (``PlanarFlow.py:20-33, 43-53``)."""
+    assert tk.shape[-1] == 2 * d + 1  # PlanarFlow.py:22
+    dt = tk.dtype
+    u = tk[..., 0:d]
+    w = tk[..., d : 2 * d] + dt.type(1)
+    b = tk[..., 2 * d : 2 * d + 1]
+    wtu = np.sum(w * u, axis=-1, keepdims=True, dtype=dt)
+    m_wtu = (dt.type(-1.0) + softplus(wtu)) + dt.type(1e-5)
+    norm_w_squared = np.sum(w**2, axis=-1, keepdims=True, dtype=dt) + dt.type(1e-9)
+    u_hat = u + (m_wtu - wtu) * (w / norm_w_squared)
+    return u_hat, w, b
+
+
+def _planar_wzb(z, w, b):
+    """``PlanarFlow._wzb`` (``PlanarFlow.py:55-59``)."""
+    return np.sum(w * z, axis=-1, keepdims=True, dtype=z.dtype) + b
+
+
+def planar_forward(z, u_hat, w, b):
+    """``PlanarFlow._forward`` (``PlanarFlow.py:68-72``)."""
+    return z + u_hat * np.tanh(_planar_wzb(z, w, b))
+
+
+def planar_fldj(z, u_hat, w, b):
+    """``PlanarFlow._forward_log_det_jacobian`` (``PlanarFlow.py:74-80``)."""
+    dt = z.dtype
+    th = np.tanh(_planar_wzb(z, w, b))
+    psi = (dt.type(1.0) - th**2) * w  # _der_tanh, PlanarFlow.py:61-66
+    det_grad = dt.type(1.0) + np.sum(u_hat * psi, axis=-1, dtype=dt)
+    with np.errstate(divide="ignore"):
+        return np.log(np.abs(det_grad))
+
+
+def radial_params(tk: np.ndarray, d: int):
+    """``RadialFlow.__init__`` + ``_alpha_circ``/``_beta_circ``
+    (``RadialFlow.py:20-34, 72-84``)."""
+    assert tk.shape[-1] == d + 2  # RadialFlow.py:23
+    dt = tk.dtype
+    alpha = softplus(dt.type(0.3) * tk[..., 0:1] - dt.type(2.0))
+    beta = softplus(dt.type(0.1) * tk[..., 1:2] + _log_expm1_one(dt)) - dt.type(1.0)
+    gamma = tk[..., 2 : d + 2]
+    return alpha, beta, gamma
+
+
+def radial_forward(z, alpha, beta, gamma):
+    """``RadialFlow._forward`` (``RadialFlow.py:44-56``); note ``_r`` is the
+    L1 norm ``sum(|z-gamma|)``."""
+    dt = z.dtype
+    r = np.sum(np.abs(z - gamma), axis=-1, keepdims=True, dtype=dt)
+    h = dt.type(1.0) / (alpha + r)
+    return z + (alpha * beta * h) * (z - gamma)
+
+
+def radial_fldj(z, alpha, beta, gamma, d: int):
+    """``RadialFlow._forward_log_det_jacobian`` (``RadialFlow.py:58-70``).
+
+    ``der_h`` is TF's ``RealDiv`` gradient of ``1/(alpha+r)``: ``((-1/y)/y)``.
+    No ``abs`` is taken (``RadialFlow.py:70``)."""
+    dt = z.dtype
+    r = np.sum(np.abs(z - gamma), axis=-1, keepdims=True, dtype=dt)
+    y = alpha + r
+    h = dt.type(1.0) / y
+    der_h = (dt.type(-1.0) / y) / y
+    ab = alpha * beta
+    det = (dt.type(1.0) + ab * h) ** dt.type(d - 1) * (dt.type(1.0) + ab * h + ab * der_h * r)
+    det = det[..., 0]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.log(det)
+
+
+def affine_params(tk: np.ndarray, d: int):
+    """``AffineFlow.__init__`` (``AffineFlow.py:5-9``)."""
+    assert tk.shape[-1] == 2 * d  # AffineFlow.py:6
+    dt = tk.dtype
+    return tk[..., 0:d], dt.type(1.0) + tk[..., d : 2 * d]
+
+
+def affine_forward(z, shift, scale):
+    """TFP ``Affine`` with diagonal scale: ``x * scale_diag + shift``."""
+    return z * scale + shift
+
+
+def affine_fldj(z, shift, scale):
+    """TFP ``Affine`` fldj: ``sum(log|scale_diag|)`` (no dependence on z)."""
+    dt = z.dtype
+    with np.errstate(divide="ignore"):
+        v = np.sum(np.log(np.abs(scale)), axis=-1, dtype=dt)
+    return np.broadcast_to(v, np.broadcast_shapes(v.shape, z.shape[:-1])).astype(dt)
+
+
+def flow_forward_fldj(flow_type: str, z: np.ndarray, tk: np.ndarray, d: int):
+    """One bijector: ``(forward(z), forward_log_det_jacobian(z))``."""
+    if flow_type == "planar":
+        u_hat, w, b = planar_params(tk, d)
+        return planar_forward(z, u_hat, w, b), planar_fldj(z, u_hat, w, b)
+    if flow_type == "radial":
+        a, be, g = radial_params(tk, d)
+        return radial_forward(z, a, be, g), radial_fldj(z, a, be, g, d)
+    if flow_type == "affine":
+        sh, sc = affine_params(tk, d)
+        return affine_forward(z, sh, sc), affine_fldj(z, sh, sc)
+    raise AssertionError(f"unknown flow type {flow_type!r}")
+
+
+# ---------------------------------------------------------------------------
+# Base distribution (``DistributionLayers.py:280-294``)
+# ---------------------------------------------------------------------------
+
+
+def base_params(base_block, d: int, trainable: bool, dt):
+    if trainable:
+        loc = base_block[..., 0:d]
+        scale = dt.type(1e-3) + softplus(_log_expm1_one(dt) + dt.type(0.1) * base_block[..., d : 2 * d])
+        return loc, scale
+    return None, None
+
+
+def base_log_prob(x: np.ndarray, loc, scale) -> np.ndarray:
+    """TFP ``MultivariateNormalDiag.log_prob``."""
+    dt = x.dtype
+    d = x.shape[-1]
+    if loc is None:
+        zz = x
+        log_det = dt.type(0.0)
+    else:
+        zz = (x - loc) / scale
+        log_det = np.sum(np.log(np.abs(scale)), axis=-1, dtype=dt)
+    unnorm = dt.type(-0.5) * np.sum(zz**2, axis=-1, dtype=dt)
+    norm = dt.type(0.5 * d * math.log(2.0 * math.pi)) + log_det
+    return unnorm - norm
+
+
+# ---------------------------------------------------------------------------
+# The hot path: TransformedDistribution(base, Invert(Chain(reversed flows)))
+# ---------------------------------------------------------------------------
+
+
+def chain_log_prob(
+    y: np.ndarray,
+    t: np.ndarray,
+    flow_types: Sequence[str],
+    d: int,
+    trainable_base: bool,
+    dtype=np.float64,
+) -> np.ndarray:
+    """``log_prob(y | t)`` — ``DistributionLayers.py:245-255`` driven by TFP.
+
+    ``y``: (B or 1, d); ``t``: (B or 1, P).  Returns (B,).
+    """
+    dt = np.dtype(dtype)
+    y = np.asarray(y, dtype=dt)
+    t = np.asarray(t, dtype=dt)
+    assert y.shape[-1] == d
+    base_block, blocks = split_params(t, flow_types, d, trainable_base)
+    B = max(y.shape[0], t.shape[0])
+    z = np.broadcast_to(y, (B, d)).astype(dt)
+    ildj = np.zeros((B,), dtype=dt)
+    for ft, tk in zip(flow_types, blocks):  # application order = flow_types order
+        z_next, fldj = flow_forward_fldj(ft, z, tk, d)
+        ildj = ildj + fldj
+        z = z_next
+    loc, scale = base_params(base_block, d, trainable_base, dt)
+    return base_log_prob(z, loc, scale) + ildj
+
+
+def normalize_y(y, y_mean, y_std, dtype=np.float64):
+    """``BaseEstimator.py:85`` — ``(y - ones_like(y)*y_mean) / y_std``."""
+    dt = np.dtype(dtype)
+    y = np.asarray(y, dtype=dt)
+    return (y - np.ones_like(y) * np.asarray(y_mean, dtype=dt)) / np.asarray(y_std, dtype=dt)
+
+
+def log_pdf(y, t, flow_types, d, trainable_base, y_mean=None, y_std=None, dtype=np.float64):
+    """``BaseEstimator.log_pdf`` (``BaseEstimator.py:77-86``) given ``t = MLP(x)``:
+    ``log_prob((y-mu)/sigma) - sum(log sigma)``.  Also equals ``-nll`` of
+    ``BaseEstimator._get_neg_log_likelihood`` (``:55-59``) at inference."""
+    dt = np.dtype(dtype)
+    if y_mean is None:
+        return chain_log_prob(y, t, flow_types, d, trainable_base, dt)
+    y_circ = normalize_y(y, y_mean, y_std, dt)
+    lp = chain_log_prob(y_circ, t, flow_types, d, trainable_base, dt)
+    return lp - np.sum(np.log(np.asarray(y_std, dtype=dt)), dtype=dt)
+
+
+def posterior_lse(y, t_draws, flow_types, d, trainable_base, y_mean=None, y_std=None, dtype=np.float64):
+    """``BayesianNNEstimator.score`` per-sample part (``BayesianNNEstimator.py:65-76``,
+    ``scorers.py:13-27``): ``logsumexp_s(-nll[s, b]) - log(S)``.  ``t_draws``: (S, B, P)."""
+    dt = np.dtype(dtype)
+    S = t_draws.shape[0]
+    scores = np.stack(
+        [log_pdf(y, t_draws[s], flow_types, d, trainable_base, y_mean, y_std, dt) for s in range(S)]
+    )
+    m = np.max(scores, axis=0)
+    lse = m + np.log(np.sum(np.exp(scores - m), axis=0))
+    return (lse - np.log(dt.type(S))).astype(dt)
+
+
+# ---------------------------------------------------------------------------
+# Parity tolerance
+# ---------------------------------------------------------------------------
+
+REL_TOL = 1e-5  # BASELINE.json north_star: "within 1e-5 relative fp32 tolerance"
+
+
+def tolerance_bound(ref64: np.ndarray, ref32: np.ndarray, rel: float = REL_TOL, cond_factor: float = 8.0):
+    """Per-sample admissible |gpu - ref64|.
+
+    ``rel * max(1, |ref|)`` — the north-star 1e-5 relative bound, with the
+    denominator floored at 1 because ``log_prob`` crosses 0 — widened, only on
+    samples where the reference's own fp32 evaluation is ill-conditioned, to
+    ``cond_factor`` times the fp32 mirror's deviation from the fp64 truth.
+    """
+    base = rel * np.maximum(1.0, np.abs(ref64))
+    cond = cond_factor * np.abs(ref32.astype(np.float64) - ref64)
+    return np.maximum(base, cond)

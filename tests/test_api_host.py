@@ -1,0 +1,114 @@
+"""Host-side API mirror of the reference (no compute): the shape / size / order /
+assertion checks of tests/test_flows.py and tests/test_distribution_layers.py,
+re-expressed against normalizingflownetwork_amd."""
+
+import numpy as np
+import pytest
+
+from normalizingflownetwork_amd import FLOWS, AffineFlow, InverseNormalizingFlowLayer, PlanarFlow, RadialFlow
+from normalizingflownetwork_amd.distribution_layers import TensorShape
+from normalizingflownetwork_amd.parallel import shard_bounds
+
+
+def test_registry():
+    assert FLOWS == {"planar": PlanarFlow, "radial": RadialFlow, "affine": AffineFlow}
+
+
+@pytest.mark.parametrize("name", ["planar", "radial", "affine"])
+def test_param_width_assertion_and_event_ndims(name):
+    # tests/test_flows.py:13-23
+    for dim in (1, 4):
+        cls = FLOWS[name]
+        with pytest.raises(AssertionError):
+            cls(np.ones((10, cls.get_param_size(dim) + 1), np.float32), dim)
+        flow = cls(np.ones((10, cls.get_param_size(dim)), np.float32), dim)
+        ref = AffineFlow(np.ones((10, AffineFlow.get_param_size(dim)), np.float32), dim)
+        assert flow.forward_min_event_ndims == ref.forward_min_event_ndims == 1
+        assert flow.inverse_min_event_ndims == 1
+
+
+def test_total_param_size_nf():
+    # tests/test_distribution_layers.py:65-73
+    layer1 = InverseNormalizingFlowLayer(("planar", "radial", "affine"), n_dims=1, trainable_base_dist=False)
+    layer2 = InverseNormalizingFlowLayer(("planar", "radial", "affine"), n_dims=3, trainable_base_dist=True)
+    assert layer1.get_total_param_size() == 3 + 3 + 2
+    assert layer2.get_total_param_size() == (3 + 3 + 1) + (3 + 1 + 1) + (3 + 3) + (3 + 3)
+
+
+def test_unknown_flow_type():
+    with pytest.raises(AssertionError):
+        InverseNormalizingFlowLayer(("planar", "banana"), n_dims=1)
+
+
+def test_nf_dist_fn_shapes():
+    # tests/test_distribution_layers.py:203-231
+    dist_fn = InverseNormalizingFlowLayer._get_distribution_fn(n_dims=1, flow_types=("radial", "planar"),
+                                                               trainable_base_dist=False)
+    dist = dist_fn(np.ones((1, 6), np.float32))
+    assert dist.event_shape == [1]
+    assert dist.batch_shape == [1]
+    dist = dist_fn(np.ones((3, 6), np.float32))
+    assert dist.event_shape == [1]
+    assert dist.batch_shape == [3]
+    with pytest.raises(AssertionError):
+        dist_fn(np.ones((10, 7), np.float32))
+    dist_fn = InverseNormalizingFlowLayer._get_distribution_fn(n_dims=2, flow_types=("radial", "planar"),
+                                                               trainable_base_dist=True)
+    dist = dist_fn(np.ones((1, 13), np.float32))
+    assert dist.event_shape == [2]
+    assert dist.batch_shape == [1]
+    dist = dist_fn(np.ones((3, 13), np.float32))
+    assert dist.event_shape == [2]
+    assert dist.batch_shape == [3]
+    with pytest.raises(AssertionError):
+        dist_fn(np.ones((10, 12), np.float32))
+
+
+def test_get_bijector_order():
+    # tests/test_distribution_layers.py:234-249
+    out = InverseNormalizingFlowLayer._get_bijector(np.zeros((10, 8), np.float32), ("planar", "radial", "affine"), 1)
+    assert len(out.bijectors) == 3
+    assert out.inverse_min_event_ndims == 1
+    assert type(out.bijectors[0]) == FLOWS["affine"]
+    assert type(out.bijectors[1]) == FLOWS["radial"]
+    assert type(out.bijectors[2]) == FLOWS["planar"]
+    out = InverseNormalizingFlowLayer._get_bijector(np.zeros((10, 9), np.float32), ("planar", "radial"), 2)
+    assert len(out.bijectors) == 2
+    assert out.inverse_min_event_ndims == 1
+    with pytest.raises(AssertionError):
+        InverseNormalizingFlowLayer._get_bijector(np.zeros((10, 8), np.float32), ("planar", "radial"), 2)
+
+
+def test_get_bijector_blocks_are_reversed():
+    """bijectors[0] (last flow type) owns the FIRST block after the base."""
+    t = np.arange(8, dtype=np.float32)[None, :]
+    chain = InverseNormalizingFlowLayer._get_bijector(t, ("planar", "radial", "affine"), 1)
+    np.testing.assert_array_equal(chain.bijectors[0]._t, [[0, 1]])  # affine (2)
+    np.testing.assert_array_equal(chain.bijectors[1]._t, [[2, 3, 4]])  # radial (3)
+    np.testing.assert_array_equal(chain.bijectors[2]._t, [[5, 6, 7]])  # planar (3)
+
+
+def test_sampling_is_impossible():
+    dist = InverseNormalizingFlowLayer(("radial",), 1, False)(np.ones((2, 3), np.float32))
+    with pytest.raises(NotImplementedError):
+        dist.sample()
+    with pytest.raises(NotImplementedError):
+        RadialFlow(np.ones((2, 3), np.float32), 1).inverse([[0.0]])
+
+
+def test_tensorshape_semantics():
+    assert TensorShape([3]) == [3]
+    assert TensorShape([3]) == (3,)
+    assert TensorShape([3]) == 3
+    assert TensorShape([3]) != [2]
+    assert hash(TensorShape([1, 2])) == hash((1, 2))
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (1 << 24, 8), (7, 8), (0, 2)])
+def test_shard_bounds_partition(n, world):
+    spans = [shard_bounds(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a, b), (c, _) in zip(spans, spans[1:]):
+        assert b == c and b >= a
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1

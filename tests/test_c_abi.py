@@ -1,0 +1,112 @@
+"""The C-ABI library loads and exports every symbol include/nfn.h declares; host-side
+validation (no GPU needed: every case here fails before any HIP call)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+from oracle import nfn_oracle as O
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "nfn.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nfn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    syms = header_symbols()
+    for s in ("nfn_chain_logprob_f32", "nfn_flow_fwd_ldj_f32", "nfn_posterior_lse_f32", "nfn_version",
+              "nfn_last_error", "nfn_param_size", "nfn_total_param_size", "nfn_set_math_mode"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol(native_lib):
+    from normalizingflownetwork_amd import _lib
+
+    for s in header_symbols():
+        assert hasattr(native_lib, s), f"{s} not exported by {_lib.LIB_NAME}"
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+    # and nothing the binding expects is missing from the header
+    assert set(_lib.SIGNATURES) == set(header_symbols())
+
+
+def test_exported_symbols_are_c_linkage(native_lib):
+    from normalizingflownetwork_amd import _lib
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (nfn_[a-z0-9_]+)$", out, flags=re.M))
+    assert set(header_symbols()) <= exported
+
+
+def test_version(native_lib):
+    assert native_lib.nfn_version() == 100
+
+
+def _ids(*names):
+    return (ctypes.c_int32 * max(1, len(names)))(*[O.FLOW_IDS[n] for n in names])
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 8, 16, 32])
+def test_param_sizes_match_python(native_lib, d):
+    for f in ("planar", "radial", "affine"):
+        assert native_lib.nfn_param_size(O.FLOW_IDS[f], d) == O.param_size(f, d)
+    ft = ("planar", "radial", "affine", "radial")
+    for tr in (0, 1):
+        assert native_lib.nfn_total_param_size(ctypes.cast(_ids(*ft), ctypes.c_void_p), len(ft), d, tr) == \
+            O.total_param_size(ft, d, bool(tr))
+
+
+def test_bad_arguments_are_rejected_before_launch(native_lib):
+    lib = native_lib
+    assert lib.nfn_param_size(7, 1) == -2
+    assert lib.nfn_param_size(0, 0) == -1
+    assert lib.nfn_param_size(0, 33) == -1
+    assert b"n_dims" in lib.nfn_last_error()
+    bad = (ctypes.c_int32 * 1)(5)
+    assert lib.nfn_total_param_size(ctypes.cast(bad, ctypes.c_void_p), 1, 1, 0) == -2
+    # too many flows
+    many = (ctypes.c_int32 * 65)(*([1] * 65))
+    assert lib.nfn_total_param_size(ctypes.cast(many, ctypes.c_void_p), 65, 1, 0) == -2
+    ids = ctypes.cast(_ids("planar", "radial"), ctypes.c_void_p)
+    fake = 0x1000  # never dereferenced: every call below fails validation first
+    # negative batch
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 8, -1, 1, ids, 2, 1, None, None, fake, None, None, None) == -1
+    # row stride smaller than P
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 4, 10, 1, ids, 2, 1, None, None, fake, None, None, None) == -1
+    # y_mean without y_std
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 8, 10, 1, ids, 2, 1, fake, None, fake, None, None, None) == -3
+    # sum requested without workspace
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 8, 10, 1, ids, 2, 1, None, None, fake, fake, None, None) == -3
+    # NULL y
+    assert lib.nfn_chain_logprob_f32(None, 1, fake, 8, 10, 1, ids, 2, 1, None, None, fake, None, None, None) == -3
+    # bad flow id in the single-flow entry point
+    assert lib.nfn_flow_fwd_ldj_f32(9, fake, 1, fake, 3, 10, 1, fake, fake, None) == -2
+    assert lib.nfn_flow_fwd_ldj_f32(0, fake, 1, fake, 2, 10, 1, fake, fake, None) == -1  # stride < 2d+1
+    # posterior with zero draws
+    assert lib.nfn_posterior_lse_f32(fake, 1, fake, 80, 8, 0, 10, 1, ids, 2, 1, None, None, fake, None, None,
+                                     None) == -1
+    assert lib.nfn_set_math_mode(3) == -1
+
+
+def test_workspace_size(native_lib):
+    assert native_lib.nfn_chain_workspace_doubles(0, 1, 32) == 0
+    assert native_lib.nfn_chain_workspace_doubles(1 << 24, 1, 32) == (1 << 24) // 256
+    assert native_lib.nfn_chain_workspace_doubles(1000, 1, 32) == 4
+    # wide rows use smaller tiles (LDS budget)
+    assert native_lib.nfn_chain_workspace_doubles(1 << 22, 8, 140) >= (1 << 22) // 256
+
+
+def test_python_binding_fails_loudly_without_device(native_lib):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible")
+    from normalizingflownetwork_amd import ops
+
+    with pytest.raises(RuntimeError):
+        ops.chain_log_prob([[0.0]], [[0.0] * 8], ("radial", "radial"), 1, True)

@@ -1,0 +1,285 @@
+"""Parity of the HIP path (through the C ABI) against the oracle.
+
+Tolerance (written once, used everywhere): ``oracle.tolerance_bound`` —
+``|gpu - ref64| <= max(1e-5 * max(1, |ref64|), 8 * |ref32 - ref64|)`` per sample:
+the north-star 1e-5 relative bound (denominator floored at 1 because log_prob
+crosses 0), widened only where the reference's own fp32 op order is
+ill-conditioned (measured by the fp32 mirror).  Both transcendental modes
+(fast = default, precise) must pass.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import CHAIN_FIXTURES, FLOW_FIXTURES, load_golden
+from oracle import nfn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+MODES = ["fast", "precise"]
+
+
+@pytest.fixture(params=MODES)
+def math_mode(request, gpu):
+    from normalizingflownetwork_amd import ops
+
+    prev = ops.set_math_mode(request.param)
+    yield request.param
+    ops.set_math_mode(prev)
+
+
+def assert_within(got, ref64, ref32, what, extra_rel=0.0):
+    got = np.asarray(got, np.float64)
+    bound = O.tolerance_bound(ref64, ref32)
+    if extra_rel:
+        bound = bound + extra_rel * np.maximum(1.0, np.abs(ref64))
+    err = np.abs(got - ref64)
+    bad = ~(err <= bound)
+    assert not bad.any(), (
+        f"{what}: {bad.sum()} / {bad.size} samples outside tolerance; worst idx {int(np.argmax(err - bound))} "
+        f"got {got[np.argmax(err - bound)]!r} ref {ref64[np.argmax(err - bound)]!r}"
+    )
+    return float((err / np.maximum(1.0, np.abs(ref64))).max())
+
+
+@pytest.mark.parametrize("name", CHAIN_FIXTURES)
+def test_chain_fixture(name, math_mode):
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden(name)
+    lp, s = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], g["d"], bool(g["trainable"]), want_sum=True)
+    lp = lp.cpu().numpy()
+    assert lp.shape == g["ref64"].shape
+    assert_within(lp, g["ref64"], g["ref32"], f"{name}/{math_mode}")
+    # the fused fp64 sum equals the sum of the returned values
+    assert float(s.item()) == pytest.approx(lp.astype(np.float64).sum(), rel=1e-12, abs=1e-9)
+
+
+def test_c1_log_pdf_with_fused_normalisation(math_mode):
+    """BaseEstimator.log_pdf (BaseEstimator.py:77-86) on the reference's own data
+    (simulation/dummy_data_gen.py cosine data, captured in the fixture)."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+
+    g = load_golden("c1_nfn_radial2_d1")
+    dist = InverseNormalizingFlowLayer(("radial", "radial"), 1, True)(g["t"])
+    lp = dist.log_prob(g["y_raw"], g["y_mean"], g["y_std"]).cpu().numpy()
+    assert_within(lp, g["logpdf64"], g["logpdf32"], "c1 log_pdf")
+
+
+@pytest.mark.parametrize("name", FLOW_FIXTURES)
+def test_single_flow_fixture(name, math_mode):
+    from normalizingflownetwork_amd import FLOWS
+
+    g = load_golden(name)
+    ftype = name.split("_")[1]
+    flow = FLOWS[ftype](g["t"], g["d"])
+    z_out, ldj = flow.forward_and_log_det_jacobian(g["z"])
+    z_out, ldj = z_out.cpu().numpy(), ldj.cpu().numpy()
+    for j in range(g["d"]):
+        assert_within(z_out[:, j], g["fwd64"][:, j], g["fwd32"][:, j], f"{name} forward[{j}]")
+    assert_within(ldj, g["ldj64"], g["ldj32"], f"{name} fldj")
+    # the separate entry points agree with the combined one
+    np.testing.assert_array_equal(flow.forward(g["z"]).cpu().numpy(), z_out)
+    np.testing.assert_array_equal(flow._forward_log_det_jacobian(g["z"]).cpu().numpy(), ldj)
+
+
+@pytest.mark.parametrize("name", ["planar", "radial"])
+def test_reference_flow_dimension_testing(name, gpu):
+    """tests/test_flows.py:10-41 on the HIP path."""
+    from normalizingflownetwork_amd import FLOWS, AffineFlow
+
+    batch_size = 10
+    for dim in (1, 4):
+        cls = FLOWS[name]
+        flow = cls(torch.ones((batch_size, cls.get_param_size(dim))), dim)
+        reference = AffineFlow(torch.ones((batch_size, AffineFlow.get_param_size(dim))), dim)
+        for tensor in ([[0.0] * dim], [[1.0] * dim] * batch_size):
+            assert flow.forward(tensor).shape == reference.forward(tensor).shape
+            assert flow._forward_log_det_jacobian(tensor).shape == reference._forward_log_det_jacobian(tensor).shape
+        tensor = [[1.0] * dim] + ([[0.0] * dim] * (batch_size - 2)) + [[1.0] * dim]
+        res = flow.forward(tensor).cpu().numpy()
+        assert res[0] == pytest.approx(res[-1], rel=1e-5)
+        assert res[1] == pytest.approx(res[-2], rel=1e-5)
+        assert not all(res[0] == res[1])
+        res = flow._forward_log_det_jacobian(tensor).cpu().numpy()
+        assert res[0] == pytest.approx(res[-1], rel=1e-5)
+        assert res[1] == pytest.approx(res[-2], rel=1e-5)
+        assert not res[0] == pytest.approx(res[1])
+        # and the values themselves against the oracle
+        g = load_golden(f"flow_{name}_d{dim}")
+        np.testing.assert_allclose(flow.forward(tensor).cpu().numpy(), g["sym_fwd64"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(res, g["sym_ldj64"], rtol=1e-5, atol=1e-6)
+
+
+def test_posterior_fixture(math_mode):
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden("posterior_s8_pr5_d1")
+    out, s = ops.posterior_lse(g["y"], g["t"], g["flow_types"], 1, True, g["y_mean"], g["y_std"], want_sum=True)
+    out = out.cpu().numpy()
+    assert_within(out, g["ref64"], g["ref32"], "posterior")
+    assert float(s.item()) == pytest.approx(out.astype(np.float64).sum(), rel=1e-12)
+
+
+def test_posterior_single_draw_equals_log_pdf(gpu):
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden("posterior_s8_pr5_d1")
+    t1 = g["t"][:1]
+    out, _ = ops.posterior_lse(g["y"], t1, g["flow_types"], 1, True, g["y_mean"], g["y_std"])
+    lp, _ = ops.chain_log_prob(g["y"], t1[0], g["flow_types"], 1, True, g["y_mean"], g["y_std"])
+    np.testing.assert_allclose(out.cpu().numpy(), lp.cpu().numpy(), rtol=0, atol=2e-6)
+
+
+def test_chain_bijector_api_matches_fused_kernel(gpu):
+    """Invert(Chain) built by _get_bijector, driven flow by flow through the
+    single-flow kernel, gives the same log_prob as the fused kernel."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+
+    g = load_golden("asym_pra_d3")
+    dist = InverseNormalizingFlowLayer(g["flow_types"], 3, True)(torch.as_tensor(g["t"]).cuda())
+    chain = dist.bijector.bijector
+    x = chain.forward(g["y"])
+    ildj = dist.bijector.inverse_log_det_jacobian(g["y"], event_ndims=1)
+    lp_steps = (dist.distribution.log_prob(x) + ildj).cpu().numpy()
+    lp_fused = dist.log_prob(g["y"]).cpu().numpy()
+    np.testing.assert_allclose(lp_steps, lp_fused, rtol=2e-5, atol=2e-5)
+    assert_within(lp_fused, g["ref64"], g["ref32"], "fused")
+
+
+def test_broadcast_and_strided_views(gpu):
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden("c2_pr5_d1")
+    ft, B = g["flow_types"], 1024
+    y, t = torch.as_tensor(g["y"][:B]).cuda(), torch.as_tensor(g["t"][:B]).cuda()
+    ref, _ = ops.chain_log_prob(y, t, ft, 1, True)
+    # t as a column slice of a wider row buffer (non-contiguous rows, stride 40)
+    wide = torch.zeros((B, 40), device="cuda")
+    wide[:, 5:37] = t
+    got, _ = ops.chain_log_prob(y, wide[:, 5:37], ft, 1, True)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref.cpu().numpy())
+    # y of batch 1 against t of batch B, and t of batch 1 against y of batch B
+    got, _ = ops.chain_log_prob(y[:1], t, ft, 1, True)
+    full, _ = ops.chain_log_prob(y[:1].expand(B, 1).contiguous(), t, ft, 1, True)
+    np.testing.assert_array_equal(got.cpu().numpy(), full.cpu().numpy())
+    got, _ = ops.chain_log_prob(y, t[:1], ft, 1, True)
+    full, _ = ops.chain_log_prob(y, t[:1].expand(B, 32).contiguous(), ft, 1, True)
+    np.testing.assert_array_equal(got.cpu().numpy(), full.cpu().numpy())
+
+
+@pytest.mark.parametrize("B", [0, 1, 63, 255, 257, 1000])
+def test_ragged_and_empty_batches(B, gpu):
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden("c2_pr5_d1")
+    ft = g["flow_types"]
+    lp, s = ops.chain_log_prob(g["y"][:B].reshape(B, 1), g["t"][:B].reshape(B, 32), ft, 1, True, want_sum=True)
+    assert lp.shape == (B,)
+    assert_within(lp.cpu().numpy(), g["ref64"][:B], g["ref32"][:B], f"B={B}")
+    assert float(s.item()) == pytest.approx(float(lp.double().sum().item()), rel=1e-12, abs=1e-12)
+
+
+def test_radial_identity_known_answer(gpu):
+    from normalizingflownetwork_amd import RadialFlow
+
+    rng = np.random.default_rng(3)
+    tk = rng.standard_normal((300, 5)).astype(np.float32)
+    tk[:, 1] = 0.0
+    z = rng.standard_normal((300, 3)).astype(np.float32)
+    zo, ldj = RadialFlow(tk, 3).forward_and_log_det_jacobian(z)
+    np.testing.assert_allclose(zo.cpu().numpy(), z, atol=1e-6)
+    np.testing.assert_allclose(ldj.cpu().numpy(), 0.0, atol=1e-6)
+
+
+def test_estimators_end_to_end(gpu):
+    from normalizingflownetwork_amd.estimators import BayesNormalizingFlowNetwork, NormalizingFlowNetwork
+    from normalizingflownetwork_amd.scorers import DummySklearWrapper, mle_log_likelihood_score
+
+    g = load_golden("c1_nfn_radial2_d1")
+    x, y = g["x"], g["y_raw"]
+    nfn = NormalizingFlowNetwork(n_dims=1, n_flows=2, hidden_sizes=(16, 16), activation="tanh")
+    nfn.set_data_normalization(x, y)
+    lp = nfn.log_pdf(x, y).cpu().numpy()
+    t = nfn.params(x).cpu().numpy()
+    ref64 = O.log_pdf(y, t, ("radial", "radial"), 1, True, nfn.y_mean, nfn.y_std)
+    ref32 = O.log_pdf(y, t, ("radial", "radial"), 1, True, nfn.y_mean, nfn.y_std, np.float32)
+    assert_within(lp, ref64, ref32, "NFN.log_pdf")
+    np.testing.assert_allclose(nfn.pdf(x, y).cpu().numpy(), np.exp(lp), rtol=1e-6)
+    score = nfn.score(x, y)
+    assert score == pytest.approx(ref64.mean(), rel=1e-5)
+    assert mle_log_likelihood_score(DummySklearWrapper(nfn), x, y) == pytest.approx(score, rel=1e-12)
+
+    bnn = BayesNormalizingFlowNetwork(n_dims=1, n_flows=2)
+    bnn.set_data_normalization(x, y)
+    bs = bnn.score(x[:512], y[:512], n_draws=4)
+    assert np.isfinite(bs)
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE sizes: size-independent properties + an oracle-checked sample.
+# ---------------------------------------------------------------------------
+
+FULL = {
+    "C2": (("planar", "radial") * 5, 1, 1 << 24),
+    "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22),
+}
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_full_size_properties(cfg, gpu):
+    from normalizingflownetwork_amd import ops
+
+    ft, d, B = FULL[cfg]
+    P = O.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(22)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    t = torch.randn((B, P), generator=gen, device="cuda")
+    lp1, s1 = ops.chain_log_prob(y, t, ft, d, True, want_sum=True)
+    lp2, s2 = ops.chain_log_prob(y, t, ft, d, True, want_sum=True)
+    # deterministic, bitwise (no atomics, fixed reduction order)
+    assert torch.equal(lp1, lp2) and torch.equal(s1, s2)
+    assert torch.isfinite(lp1).all()
+    # fused fp64 sum == sum of outputs
+    assert float(s1.item()) == pytest.approx(float(lp1.double().sum().item()), rel=1e-12)
+    # sum-only launch gives the same sum
+    _, s3 = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
+    assert torch.equal(s1, s3)
+    # samples are independent: a permutation of the batch permutes the outputs bitwise
+    perm = torch.randperm(B, generator=gen, device="cuda")
+    lpp, _ = ops.chain_log_prob(y[perm], t[perm], ft, d, True)
+    assert torch.equal(lpp, lp1[perm])
+    # 4096 random samples (spread over the whole batch) against the oracle
+    for what, idx in (("sample", torch.randint(0, B, (4096,), generator=gen, device="cuda")),
+                      ("tail", torch.arange(B - 300, B, device="cuda"))):
+        yn, tn = y[idx].cpu().numpy(), t[idx].cpu().numpy()
+        ref64 = O.chain_log_prob(yn, tn, ft, d, True, np.float64)
+        ref32 = O.chain_log_prob(yn, tn, ft, d, True, np.float32)
+        assert_within(lp1[idx].cpu().numpy(), ref64, ref32, f"{cfg} {what}")
+
+
+def test_full_size_posterior_properties(gpu):
+    """C5 shape per GPU (S=64, B=2^17): lse of identical draws == single-draw log_prob."""
+    from normalizingflownetwork_amd import ops
+
+    ft = ("planar", "radial") * 5
+    S, B = 64, 1 << 17
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    y = torch.randn((B, 1), generator=gen, device="cuda")
+    t = torch.randn((S, B, 32), generator=gen, device="cuda")
+    out, s = ops.posterior_lse(y, t, ft, 1, True, want_sum=True)
+    assert torch.isfinite(out).all()
+    assert float(s.item()) == pytest.approx(float(out.double().sum().item()), rel=1e-12)
+    idx = torch.randint(0, B, (256,), generator=gen, device="cuda")
+    tn, yn = t[:, idx].cpu().numpy(), y[idx].cpu().numpy()
+    ref64 = O.posterior_lse(yn, tn, ft, 1, True)
+    ref32 = O.posterior_lse(yn, tn, ft, 1, True, dtype=np.float32)
+    assert_within(out[idx].cpu().numpy(), ref64, ref32, "C5 sample")
+    # S copies of one draw: lse - log S == log_prob
+    rep = t[:1].expand(S, B, 32).contiguous()
+    out_rep, _ = ops.posterior_lse(y, rep, ft, 1, True)
+    lp, _ = ops.chain_log_prob(y, t[0], ft, 1, True)
+    np.testing.assert_allclose(out_rep.cpu().numpy(), lp.cpu().numpy(), rtol=1e-5, atol=2e-5)

@@ -1,0 +1,59 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace stats
+# (and optionally PMC passes).  Every GPU step has its own time limit; the
+# session stops at the first crash-like exit (fault/abort/segv/timeout).
+#   usage: bash tools/gpu_session.sh <tag> [tests|smoke|bench|prof|pmc|c3|c5 ...]
+set -o pipefail
+TAG=${1:-r01}; shift
+STEPS=${*:-tests smoke bench prof}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+crashed() {  # exit codes that mean "stop using the GPU in this call"
+  case $1 in 124|134|137|139) return 0;; esac
+  [ "$1" -gt 128 ] && return 0
+  return 1
+}
+
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 15 "$OUT/$name.log"
+  if crashed $rc; then echo "!!! $name crashed (rc=$rc); stopping GPU work" | tee -a "$OUT/session.log"; exit $rc; fi
+  return 0
+}
+
+rocm-smi --showproductname > "$OUT/rocm_smi.txt" 2>&1 || true
+nproc > "$OUT/nproc.txt"; lscpu > "$OUT/lscpu.txt" 2>&1 || true
+
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 1100 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 50 --warmup 10 ;;
+    bench_nocpu) run bench_nocpu 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
+    c3) run bench_c3 300 python bench.py --config C3 --steps 50 --warmup 10 --no-cpu-baseline ;;
+    c5) run bench_c5 300 python bench.py --config C5 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof)
+      { cd /tmp; run rocprof_c2 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c2" -o c2 -- \
+        python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    prof_c3)
+      { cd /tmp; run rocprof_c3 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c3" -o c3 -- \
+        python3 "$ROOT/bench.py" --config C3 --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc)
+      { cd /tmp; run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o f -- \
+        python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o w -- \
+        python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    micro) run micro 600 python tools/microbench.py ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "session done"
