@@ -28,6 +28,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 
 #include "nfn.h"
@@ -66,6 +67,8 @@ struct ChainArgs {
   int32_t trainable;
   int32_t S;           // posterior draws (1 for the plain chain)
   int32_t vec4;        // tile rows can be streamed as float4
+  int32_t ownrow;      // persistent kernel: each lane streams its own row (else cooperative)
+  int64_t ntiles;      // persistent kernel: number of `blockDim.x`-row tiles
   FlowProgram prog;
 };
 
@@ -97,6 +100,20 @@ template <bool FAST>
 __device__ __forceinline__ float f_div(float a, float b) {
   if constexpr (FAST) {
     return a * __builtin_amdgcn_rcpf(b);
+  } else {
+    return a / b;
+  }
+}
+
+// a / b correctly rounded in practice (rcp + one Newton step): used where the
+// reference's own arithmetic cancels afterwards (planar u_hat), so the 1-ulp
+// v_rcp_f32 error would be amplified.
+template <bool FAST>
+__device__ __forceinline__ float f_div_acc(float a, float b) {
+  if constexpr (FAST) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    const float q = a * r;
+    return fmaf(fmaf(-b, q, a), r, q);
   } else {
     return a / b;
   }
@@ -175,7 +192,7 @@ __device__ __forceinline__ float planar_step(float (&z)[DM], PTR p, int d) {
 #pragma unroll
   for (int j = 0; j < DM; ++j) {
     if (j < d) {
-      const float uh = u[j] + coef * f_div<FAST>(w[j], norm_w2);
+      const float uh = u[j] + coef * f_div_acc<FAST>(w[j], norm_w2);
       z[j] = z[j] + uh * th;
       s += uh * (dth * w[j]);
     }
@@ -428,6 +445,122 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
   }
 }
 
+// Persistent, software-pipelined version of the two kernels above (the hot path).
+// Each workgroup walks tiles blockIdx.x, blockIdx.x + gridDim.x, ...; for every
+// (tile, draw) unit the NEXT unit's parameter rows are already in flight in
+// registers (`buf`) while the current unit is evaluated from LDS, so HBM loads
+// never wait on the flow math.  Rows are moved as float4 (Q = P/4 per row); a
+// thread owns Q float4 slots whose addresses are affine in the slot index:
+//   cooperative (ownrow = 0, needs Q | T): slot k = float4 (tid % Q) of row
+//     tid / Q + k * T / Q — each wave instruction reads 1 KiB contiguous;
+//   own-row (ownrow = 1): slot k = float4 k of row tid — each lane streams its
+//     own row, no workgroup barrier is needed at all.
+template <int DM, bool FAST, int NV, bool POST>
+__global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  const int T = blockDim.x;
+  const int tid = threadIdx.x;
+  const int Q = a.P >> 2;
+  const int S = a.lds_stride;
+  const int64_t rs = a.t_rowstride;
+  const bool own = a.ownrow != 0;
+  const int r0 = own ? tid : tid / Q;
+  const int c4 = own ? 0 : tid - (tid / Q) * Q;
+  const int rstep = own ? 0 : T / Q;
+  const int64_t g0 = (int64_t)r0 * rs + 4 * c4;
+  const int64_t gstep = own ? 4 : (int64_t)rstep * rs;
+  const int l0 = r0 * S + 4 * c4;
+  const int lstep = own ? 4 : rstep * S;
+  const int ndraw = POST ? a.S : 1;
+
+  float4 buf[NV];
+  float ybuf[DM];
+  auto issue = [&](int64_t tile, int s) {
+    const int64_t b0 = tile * T;
+    const int nr = (int)min((int64_t)T, a.B - b0);
+    const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      if (k < Q && r0 + k * rstep < nr) buf[k] = *reinterpret_cast<const float4*>(base + g0 + k * gstep);
+    }
+    if (s == 0 && tid < nr) {
+      const float* yr = a.y + (b0 + tid) * a.y_bstride;
+#pragma unroll
+      for (int j = 0; j < DM; ++j) ybuf[j] = (j < a.d) ? yr[j] : 0.0f;
+    }
+  };
+
+  // -sum(log y_std) and the normalisation constants are per launch
+  float corr = 0.0f;
+  if (a.y_mean) {
+    for (int j = 0; j < a.d; ++j) corr += f_log<FAST>(a.y_std[j]);
+  }
+
+  double acc = 0.0;
+  int64_t tile = blockIdx.x;
+  if (tile < a.ntiles) issue(tile, 0);
+  for (; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * T;
+    const int nr = (int)min((int64_t)T, a.B - b0);
+    float z0[DM];
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+      z0[j] = ybuf[j];
+      if (a.y_mean && j < a.d) z0[j] = f_div<FAST>(z0[j] - a.y_mean[j], a.y_std[j]);
+    }
+    float m = -INFINITY, accl = 0.0f, lp = 0.0f;
+    for (int s = 0; s < ndraw; ++s) {
+      if (!own) __syncthreads();  // previous unit's LDS rows fully consumed
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (k < Q && r0 + k * rstep < nr) {
+          float* dst = lds + l0 + k * lstep;
+          dst[0] = buf[k].x;
+          dst[1] = buf[k].y;
+          dst[2] = buf[k].z;
+          dst[3] = buf[k].w;
+        }
+      }
+      if (!own) __syncthreads();
+      // prefetch the next unit while this one is evaluated
+      if (s + 1 < ndraw)
+        issue(tile, s + 1);
+      else if (tile + gridDim.x < a.ntiles)
+        issue(tile + gridDim.x, 0);
+      if (tid < nr) {
+        float z[DM];
+#pragma unroll
+        for (int j = 0; j < DM; ++j) z[j] = z0[j];
+        lp = eval_chain<DM, FAST>(z, lds + tid * S, a) - corr;
+        if constexpr (POST) {
+          if (lp > m) {
+            accl = (m == -INFINITY ? 0.0f : accl * f_exp<FAST>(m - lp)) + 1.0f;
+            m = lp;
+          } else if (lp > -INFINITY) {
+            accl += f_exp<FAST>(lp - m);
+          } else if (lp != lp) {
+            m = lp;
+          }
+        }
+      }
+    }
+    if (tid < nr) {
+      float res = lp;
+      if constexpr (POST) {
+        res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
+        res = res - f_log<FAST>((float)ndraw);
+      }
+      if (a.out) a.out[b0 + tid] = res;
+      acc += (double)res;
+    }
+  }
+  if (a.partials) {
+    const double sum = block_sum(acc, red);
+    if (tid == 0) a.partials[blockIdx.x] = sum;
+  }
+}
+
 // Single bijector over a batch (the per-flow Bijector API).  Parameters are read
 // straight from global memory: this path serves the Python Bijector objects,
 // not the fused chain.
@@ -454,8 +587,20 @@ __global__ void __launch_bounds__(kMaxBlock)
 __global__ void __launch_bounds__(1024) reduce_f64_kernel(const double* __restrict__ in, int64_t n,
                                                           double* __restrict__ out) {
   __shared__ double red[1024 / 64];
+  constexpr int U = 8;  // independent loads in flight per thread
+  double acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.0;
+  const int64_t step = (int64_t)blockDim.x * U;
+  int64_t i = threadIdx.x;
+  for (; i + (U - 1) * (int64_t)blockDim.x < n; i += step) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] += in[i + u * (int64_t)blockDim.x];
+  }
+  for (; i < n; i += blockDim.x) acc[0] += in[i];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += in[i];
+#pragma unroll
+  for (int u = 0; u < U; ++u) s += acc[u];
   s = block_sum(s, red);
   if (threadIdx.x == 0) out[0] = s;
 }
@@ -531,6 +676,68 @@ TileGeom tile_geom(int P) {
   return g;
 }
 
+// Tuning knobs (environment, read once): NFN_LOAD_MODE = auto|coop|ownrow|tile,
+// NFN_WG_PER_CU = workgroups per CU for the persistent kernel (0 = occupancy max).
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+enum LoadMode { kAuto = 0, kCoop = 1, kOwnRow = 2, kTile = 3 };
+
+int load_mode_env() {
+  const char* e = getenv("NFN_LOAD_MODE");
+  if (!e) return kAuto;
+  if (!strcmp(e, "coop")) return kCoop;
+  if (!strcmp(e, "ownrow")) return kOwnRow;
+  if (!strcmp(e, "tile")) return kTile;
+  return kAuto;
+}
+
+int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  return n;
+}
+
+template <int DM, bool FAST, int NV, bool POST>
+void launch_persistent(const ChainArgs& a0, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
+  ChainArgs a = a0;
+  auto kfn = chain_persistent_kernel<DM, FAST, NV, POST>;
+  int occ = env_int("NFN_WG_PER_CU", 0);
+  if (occ <= 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, T, lds) != hipSuccess || occ <= 0) occ = 1;
+  }
+  const int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)cu_count() * occ);
+  *grid_out = grid;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
+}
+
+template <int DM, bool FAST, bool POST>
+void launch_persistent_nv(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
+  if (Q <= 2)
+    launch_persistent<DM, FAST, 2, POST>(a, T, lds, s, g);
+  else if (Q <= 4)
+    launch_persistent<DM, FAST, 4, POST>(a, T, lds, s, g);
+  else if (Q <= 8)
+    launch_persistent<DM, FAST, 8, POST>(a, T, lds, s, g);
+  else
+    launch_persistent<DM, FAST, 16, POST>(a, T, lds, s, g);
+}
+
+template <bool FAST, bool POST>
+void launch_persistent_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
+  switch (dm) {
+    case 1: launch_persistent_nv<1, FAST, POST>(Q, a, T, lds, s, g); break;
+    case 2: launch_persistent_nv<2, FAST, POST>(Q, a, T, lds, s, g); break;
+    case 4: launch_persistent_nv<4, FAST, POST>(Q, a, T, lds, s, g); break;
+    case 8: launch_persistent_nv<8, FAST, POST>(Q, a, T, lds, s, g); break;
+    case 16: launch_persistent_nv<16, FAST, POST>(Q, a, T, lds, s, g); break;
+    default: launch_persistent_nv<32, FAST, POST>(Q, a, T, lds, s, g); break;
+  }
+}
+
 template <int DM, bool FAST>
 void launch_chain(const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool posterior) {
   if (posterior)
@@ -603,15 +810,32 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   a.S = posterior ? S : 1;
   a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((t_drawstride & 3) == 0) &&
            ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
-  const int64_t nblk = (B + g.rows - 1) / g.rows;
+  int64_t nblk = (B + g.rows - 1) / g.rows;
   if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
-  const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
   const int dm = dm_for(d);
-  if (use_fast_math())
-    launch_chain_dm<true>(dm, a, grid, block, g.lds_bytes, s, posterior);
-  else
-    launch_chain_dm<false>(dm, a, grid, block, g.lds_bytes, s, posterior);
-  int32_t rc = check_hip(posterior ? "posterior_lse_kernel launch" : "chain_logprob_kernel launch");
+  const int Q = P >> 2;
+  const int mode = load_mode_env();
+  const bool persistent = a.vec4 && t_rowstride != 0 && Q >= 1 && Q <= 16 && mode != kTile;
+  if (persistent) {
+    const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;
+    a.ownrow = (mode == kOwnRow || !coop_ok) ? 1 : 0;
+    a.ntiles = nblk;
+    const bool fast = use_fast_math();
+    if (posterior) {
+      if (fast) launch_persistent_dm<true, true>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+      else launch_persistent_dm<false, true>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+    } else {
+      if (fast) launch_persistent_dm<true, false>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+      else launch_persistent_dm<false, false>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+    }
+  } else {
+    const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
+    if (use_fast_math())
+      launch_chain_dm<true>(dm, a, grid, block, g.lds_bytes, s, posterior);
+    else
+      launch_chain_dm<false>(dm, a, grid, block, g.lds_bytes, s, posterior);
+  }
+  int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
   if (rc != NFN_OK) return rc;
   if (out_sum) {
     hipLaunchKernelGGL(reduce_f64_kernel, dim3(1), dim3(1024), 0, s, (const double*)workspace, nblk, out_sum);

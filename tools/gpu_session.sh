@@ -35,14 +35,14 @@ nproc > "$OUT/nproc.txt"; lscpu > "$OUT/lscpu.txt" 2>&1 || true
 
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 1100 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run bench 600 python bench.py --steps 50 --warmup 10 ;;
+    tests) run pytest_gpu 480 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 240 python bench.py --steps 50 --warmup 10 ;;
     bench_nocpu) run bench_nocpu 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
     c3) run bench_c3 300 python bench.py --config C3 --steps 50 --warmup 10 --no-cpu-baseline ;;
     c5) run bench_c5 300 python bench.py --config C5 --steps 20 --warmup 5 --no-cpu-baseline ;;
     prof)
-      { cd /tmp; run rocprof_c2 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c2" -o c2 -- \
+      { cd /tmp; run rocprof_c2 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c2" -o c2 -- \
         python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
     prof_c3)
       { cd /tmp; run rocprof_c3 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c3" -o c3 -- \

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of kernel variants in ONE process (cdna guide §5.4 rule 24).
+
+Variants are selected through the library's tuning environment variables
+(NFN_LOAD_MODE, NFN_WG_PER_CU) and the math mode; each round times every variant
+back to back with HIP events on the launch stream.  Outputs are also checked
+against the first variant (max |diff|)."""
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from normalizingflownetwork_amd import ops  # noqa: E402
+
+CFG = {
+    "C2": (("planar", "radial") * 5, 1, 1 << 24, None),
+    "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22, None),
+    "C5": (("planar", "radial") * 5, 1, 1 << 17, 64),
+    "C1": (("radial", "radial"), 1, 1 << 24, None),
+}
+
+
+def bytes_per_launch(d, P, B, S):
+    return B * (4 * d + 4 * P + 4) if S is None else B * (S * 4 * P + 4 * d + 4)
+
+
+def run(cfg, variants, reps=20, rounds=3):
+    ft, d, B, S = CFG[cfg]
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device="cuda")
+    L = ops.ChainLauncher(y, t, ft, d, True, draws=S)
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    times = {v["name"]: [] for v in variants}
+    outs = {}
+    for r in range(rounds):
+        for v in variants:
+            for k, val in v.get("env", {}).items():
+                os.environ[k] = str(val)
+            ops.set_math_mode(v.get("math", "fast"))
+            for _ in range(3):
+                L.launch(sh)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in evs:
+                e0.record(stream)
+                L.launch(sh)
+                e1.record(stream)
+            torch.cuda.synchronize()
+            times[v["name"]].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+            if r == 0:
+                outs[v["name"]] = L.out.clone()
+            for k in v.get("env", {}):
+                os.environ.pop(k, None)
+    ref = outs[variants[0]["name"]]
+    res = []
+    bpl = bytes_per_launch(d, P, B, S)
+    for v in variants:
+        ms = float(np.median(times[v["name"]]))
+        diff = float((outs[v["name"]] - ref).abs().max().item())
+        res.append({"cfg": cfg, "variant": v["name"], "ms": ms, "GBps": bpl / ms / 1e6, "frac8TBs": bpl / ms / 1e6 / 8000,
+                    "evals_per_s": B * (S or 1) / ms * 1e3, "maxdiff_vs_first": diff, "rounds_ms": times[v["name"]]})
+        print(json.dumps(res[-1]), flush=True)
+    return res
+
+
+def main():
+    which = sys.argv[1:] or ["C2"]
+    base = [
+        {"name": "auto", "env": {}},
+        {"name": "coop", "env": {"NFN_LOAD_MODE": "coop"}},
+        {"name": "ownrow", "env": {"NFN_LOAD_MODE": "ownrow"}},
+        {"name": "tile", "env": {"NFN_LOAD_MODE": "tile"}},
+        {"name": "coop_wg2", "env": {"NFN_LOAD_MODE": "coop", "NFN_WG_PER_CU": 2}},
+        {"name": "coop_wg3", "env": {"NFN_LOAD_MODE": "coop", "NFN_WG_PER_CU": 3}},
+        {"name": "ownrow_wg2", "env": {"NFN_LOAD_MODE": "ownrow", "NFN_WG_PER_CU": 2}},
+        {"name": "precise", "math": "precise"},
+    ]
+    for cfg in which:
+        run(cfg, base if cfg in ("C2", "C1") else [base[0], base[3], base[-1]])
+
+
+if __name__ == "__main__":
+    main()
