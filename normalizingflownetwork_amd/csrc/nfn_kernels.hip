@@ -670,6 +670,10 @@ TileGeom tile_geom(int P) {
   g.lds_stride = P | 1;  // odd stride: conflict-free per-lane ds_read_b32
   const size_t row_bytes = (size_t)g.lds_stride * sizeof(float);
   int rows = kMaxBlock;
+  if (const char* e = getenv("NFN_TILE_ROWS")) {  // tuning knob: 64, 128, 192 or 256
+    const int r = atoi(e);
+    if (r >= 64 && r <= kMaxBlock && r % 64 == 0) rows = r;
+  }
   while (rows > 64 && (size_t)rows * row_bytes > (size_t)kLdsTileBudget) rows -= 64;
   g.rows = rows;
   g.lds_bytes = P > 0 ? (size_t)rows * row_bytes : 0;
@@ -764,8 +768,6 @@ int32_t check_hip(const char* what) {
   return NFN_OK;
 }
 
-int64_t n_tiles(int64_t B, int P) { return (B + tile_geom(P).rows - 1) / tile_geom(P).rows; }
-
 int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride, int64_t t_rowstride,
                   int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
                   const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
@@ -775,6 +777,9 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   memset(&a, 0, sizeof(a));
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
   if (P < 0) return P;
+  // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
+  // the flow math, to measure the memory path of the kernel structure alone.
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
   if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
@@ -879,8 +884,9 @@ int32_t nfn_total_param_size(const int32_t* flow_ids, int32_t K, int32_t d, int3
 
 int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   (void)d;
+  (void)P;
   if (B <= 0) return 0;
-  return n_tiles(B, P < 0 ? 0 : P);
+  return (B + 63) / 64;  // one partial per workgroup at the smallest tile (64 rows)
 }
 
 int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {

@@ -52,7 +52,7 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o w -- \
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
-    micro) run micro 600 python tools/microbench.py ;;
+    micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -80,9 +80,13 @@ def main():
         {"name": "coop_wg3", "env": {"NFN_LOAD_MODE": "coop", "NFN_WG_PER_CU": 3}},
         {"name": "ownrow_wg2", "env": {"NFN_LOAD_MODE": "ownrow", "NFN_WG_PER_CU": 2}},
         {"name": "precise", "math": "precise"},
+        {"name": "ablate_flows", "env": {"NFN_ABLATE_FLOWS": 1}},
+        {"name": "coop_rows128", "env": {"NFN_LOAD_MODE": "coop", "NFN_TILE_ROWS": 128}},
+        {"name": "coop_rows192", "env": {"NFN_LOAD_MODE": "coop", "NFN_TILE_ROWS": 192}},
+        {"name": "rows128_ablate", "env": {"NFN_TILE_ROWS": 128, "NFN_ABLATE_FLOWS": 1}},
     ]
     for cfg in which:
-        run(cfg, base if cfg in ("C2", "C1") else [base[0], base[3], base[-1]])
+        run(cfg, base if cfg in ("C2", "C1") else [b for b in base if b["name"] in ("auto", "tile", "precise", "ablate_flows")])
 
 
 if __name__ == "__main__":
