@@ -498,6 +498,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
   }
 
   double acc = 0.0;
+  // The store of a tile's results is deferred to the next iteration and issued
+  // BEFORE that iteration's prefetch: vmcnt counts stores and loads in issue
+  // order, so a store issued after the prefetch would make the next wait for the
+  // prefetched rows also wait for the store's full latency.
+  int64_t pend_b = -1;
+  float pend_v = 0.0f;
   int64_t tile = blockIdx.x;
   if (tile < a.ntiles) issue(tile, 0);
   for (; tile < a.ntiles; tile += gridDim.x) {
@@ -523,6 +529,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
         }
       }
       if (!own) __syncthreads();
+      if (pend_b >= 0) {
+        if (a.out) a.out[pend_b] = pend_v;
+        pend_b = -1;
+      }
       // prefetch the next unit while this one is evaluated
       if (s + 1 < ndraw)
         issue(tile, s + 1);
@@ -551,10 +561,203 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
         res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
         res = res - f_log<FAST>((float)ndraw);
       }
-      if (a.out) a.out[b0 + tid] = res;
+      pend_b = b0 + tid;
+      pend_v = res;
       acc += (double)res;
     }
   }
+  if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
+  if (a.partials) {
+    const double sum = block_sum(acc, red);
+    if (tid == 0) a.partials[blockIdx.x] = sum;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Lane-group kernel for wide events (d >= 4; config C3 is d = 8, P = 140).
+// G = DM lanes cooperate on one sample and lane j owns z_j, so a 560-byte
+// parameter row is spread over 8 lanes instead of one: per-thread prefetch stays
+// at ceil(P / 4G) float4 and the LDS tile at (256 / G) rows, which keeps ~32
+// waves per CU resident.  The inner products of the flows (w.u, |w|^2, w.z,
+// u_hat.psi, |z - gamma|_1) are xor-shuffle reductions inside the G-lane group;
+// per-sample scalars (softplus, tanh, log det) are evaluated redundantly by the
+// group's lanes.  Per-dimension log terms (affine log|s_j|, the base density)
+// are accumulated per lane and reduced once at the end.
+// ---------------------------------------------------------------------------
+
+template <int G>
+__device__ __forceinline__ float gsum(float v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, G);
+  return v;
+}
+
+template <int G, bool FAST>
+__device__ __forceinline__ float planar_step_g(float& z, const float* p, int d, int j, bool act) {
+  const float u = act ? p[j] : 0.0f;
+  const float w = act ? p[d + j] + 1.0f : 0.0f;
+  const float wtu = gsum<G>(w * u);
+  const float nw2 = gsum<G>(w * w);
+  const float wz = gsum<G>(w * z);
+  const float b = p[2 * d];
+  const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
+  const float norm_w2 = nw2 + 1e-9f;
+  const float coef = m_wtu - wtu;
+  const float th = f_tanh<FAST>(wz + b);
+  const float dth = 1.0f - th * th;
+  const float uh = u + coef * f_div_acc<FAST>(w, norm_w2);  // 0 on inactive lanes
+  z = z + uh * th;
+  const float sdet = gsum<G>(uh * (dth * w));
+  return f_log<FAST>(fabsf(1.0f + sdet));
+}
+
+template <int G, bool FAST>
+__device__ __forceinline__ float radial_step_g(float& z, const float* p, int d, int j, bool act) {
+  const float alpha = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
+  const float beta = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
+  const float g = act ? p[2 + j] : 0.0f;
+  const float r = gsum<G>(act ? fabsf(z - g) : 0.0f);
+  const float yv = alpha + r;
+  float h, der_h;
+  if constexpr (FAST) {
+    h = __builtin_amdgcn_rcpf(yv);
+    der_h = -h * h;
+  } else {
+    h = 1.0f / yv;
+    der_h = (-1.0f / yv) / yv;
+  }
+  const float ab = alpha * beta;
+  const float abh = ab * h;
+  if (act) z = z + abh * (z - g);
+  const float A = 1.0f + abh;
+  const float Bv = A + (ab * der_h) * r;
+  float Ap = 1.0f;
+  for (int i = 1; i < d; ++i) Ap *= A;
+  return f_log<FAST>(Ap * Bv);
+}
+
+template <int G, bool FAST>
+__device__ __forceinline__ float eval_chain_g(float z, const float* row, const ChainArgs& a, int j) {
+  const int d = a.d;
+  const bool act = j < d;
+  float ildj = 0.0f, dimterm = 0.0f;
+  for (int k = 0; k < a.prog.K; ++k) {
+    const int st = a.prog.step[k];
+    const float* p = row + (st >> 2);
+    const int id = st & 3;
+    if (id == NFN_FLOW_PLANAR) {
+      ildj = ildj + planar_step_g<G, FAST>(z, p, d, j, act);
+    } else if (id == NFN_FLOW_RADIAL) {
+      ildj = ildj + radial_step_g<G, FAST>(z, p, d, j, act);
+    } else if (act) {  // affine: per-dimension log|scale_j|
+      const float sc = 1.0f + p[d + j];
+      z = z * sc + p[j];
+      dimterm += f_log<FAST>(fabsf(sc));
+    }
+  }
+  if (act) {
+    if (a.trainable) {
+      const float sc = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + j]);
+      const float zz = f_div<FAST>(z - row[j], sc);
+      dimterm += -0.5f * (zz * zz) - f_log<FAST>(sc);
+    } else {
+      dimterm += -0.5f * (z * z);
+    }
+  }
+  return (gsum<G>(dimterm) - kHalfLog2Pi * (float)d) + ildj;
+}
+
+template <int G, bool FAST, int NV, bool POST>
+__global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  const int T = blockDim.x;
+  const int R = T / G;  // samples per tile
+  const int tid = threadIdx.x;
+  const int sl = tid / G;
+  const int j = tid - sl * G;
+  const int Q = a.P >> 2;
+  const int S = a.lds_stride;
+  const int64_t rs = a.t_rowstride;
+  const int ndraw = POST ? a.S : 1;
+  // tile-invariant slot map: slot k = float4 (tid + k*T) of the tile
+  int srow[NV], goff[NV], loff[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = tid + k * T;
+    const int r = q / Q, c = q - (q / Q) * Q;
+    srow[k] = (q < R * Q) ? r : 0x7fffffff;
+    goff[k] = (int)(r * rs) + 4 * c;
+    loff[k] = r * S + 4 * c;
+  }
+  float4 buf[NV];
+  float ybuf = 0.0f;
+  auto issue = [&](int64_t tile, int s) {
+    const int64_t b0 = tile * R;
+    const int nr = (int)min((int64_t)R, a.B - b0);
+    const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      if (srow[k] < nr) buf[k] = *reinterpret_cast<const float4*>(base + goff[k]);
+    }
+    if (s == 0 && sl < nr && j < a.d) ybuf = a.y[(b0 + sl) * a.y_bstride + j];
+  };
+  float corr = 0.0f;
+  if (a.y_mean) {
+    for (int i = 0; i < a.d; ++i) corr += f_log<FAST>(a.y_std[i]);
+  }
+  double acc = 0.0;
+  int64_t pend_b = -1;  // deferred store, see chain_persistent_kernel
+  float pend_v = 0.0f;
+  int64_t tile = blockIdx.x;
+  if (tile < a.ntiles) issue(tile, 0);
+  for (; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * R;
+    const int nr = (int)min((int64_t)R, a.B - b0);
+    float z0 = ybuf;
+    if (a.y_mean && j < a.d) z0 = f_div<FAST>(z0 - a.y_mean[j], a.y_std[j]);
+    float m = -INFINITY, accl = 0.0f, lp = 0.0f;
+    for (int s = 0; s < ndraw; ++s) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (srow[k] < nr) *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
+      }
+      __syncthreads();
+      if (pend_b >= 0) {
+        if (a.out) a.out[pend_b] = pend_v;
+        pend_b = -1;
+      }
+      if (s + 1 < ndraw)
+        issue(tile, s + 1);
+      else if (tile + gridDim.x < a.ntiles)
+        issue(tile + gridDim.x, 0);
+      if (sl < nr) {
+        lp = eval_chain_g<G, FAST>(z0, lds + sl * S, a, j) - corr;
+        if constexpr (POST) {
+          if (lp > m) {
+            accl = (m == -INFINITY ? 0.0f : accl * f_exp<FAST>(m - lp)) + 1.0f;
+            m = lp;
+          } else if (lp > -INFINITY) {
+            accl += f_exp<FAST>(lp - m);
+          } else if (lp != lp) {
+            m = lp;
+          }
+        }
+      }
+    }
+    if (sl < nr && j == 0) {
+      float res = lp;
+      if constexpr (POST) {
+        res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
+        res = res - f_log<FAST>((float)ndraw);
+      }
+      pend_b = b0 + sl;
+      pend_v = res;
+      acc += (double)res;
+    }
+  }
+  if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
   if (a.partials) {
     const double sum = block_sum(acc, red);
     if (tid == 0) a.partials[blockIdx.x] = sum;
@@ -742,6 +945,54 @@ void launch_persistent_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, 
   }
 }
 
+// Group kernel geometry: R = 256 / G samples per tile; LDS row stride S >= P with
+// S % G == 0 and S / G odd, so the 32 / G samples of a half-wave start on
+// distinct G-bank groups (conflict-free per-dimension ds_read_b32), and S % 4 == 0
+// for the float4 LDS writes.
+int group_lds_stride(int P, int G) {
+  int Sx = ((P + G - 1) / G) * G;
+  if (((Sx / G) & 1) == 0) Sx += G;
+  while (Sx % 4) Sx += 2 * G;
+  return Sx;
+}
+
+template <int G, bool FAST, int NV, bool POST>
+void launch_group(const ChainArgs& a0, size_t lds, hipStream_t s, int64_t* grid_out) {
+  ChainArgs a = a0;
+  auto kfn = chain_group_kernel<G, FAST, NV, POST>;
+  int occ = env_int("NFN_WG_PER_CU", 0);
+  if (occ <= 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, kMaxBlock, lds) != hipSuccess || occ <= 0) occ = 1;
+  }
+  const int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)cu_count() * occ);
+  *grid_out = grid;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+}
+
+template <int G, bool FAST, bool POST>
+void launch_group_nv(int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
+  if (nv <= 2)
+    launch_group<G, FAST, 2, POST>(a, lds, s, g);
+  else if (nv <= 4)
+    launch_group<G, FAST, 4, POST>(a, lds, s, g);
+  else if (nv <= 6)
+    launch_group<G, FAST, 6, POST>(a, lds, s, g);
+  else if (nv <= 8)
+    launch_group<G, FAST, 8, POST>(a, lds, s, g);
+  else
+    launch_group<G, FAST, 16, POST>(a, lds, s, g);
+}
+
+template <bool FAST, bool POST>
+void launch_group_g(int G, int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
+  switch (G) {
+    case 4: launch_group_nv<4, FAST, POST>(nv, a, lds, s, g); break;
+    case 8: launch_group_nv<8, FAST, POST>(nv, a, lds, s, g); break;
+    case 16: launch_group_nv<16, FAST, POST>(nv, a, lds, s, g); break;
+    default: launch_group_nv<32, FAST, POST>(nv, a, lds, s, g); break;
+  }
+}
+
 template <int DM, bool FAST>
 void launch_chain(const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool posterior) {
   if (posterior)
@@ -820,8 +1071,25 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   const int dm = dm_for(d);
   const int Q = P >> 2;
   const int mode = load_mode_env();
-  const bool persistent = a.vec4 && t_rowstride != 0 && Q >= 1 && Q <= 16 && mode != kTile;
-  if (persistent) {
+  const int G = dm;  // lanes per sample for the group kernel
+  const int nv_group = (Q + G - 1) / G;
+  const bool group = a.vec4 && t_rowstride != 0 && d >= 4 && Q >= 1 && nv_group <= 16 && mode != kTile &&
+                     mode != kCoop && mode != kOwnRow && env_int("NFN_GROUP", 1) != 0;
+  const bool persistent = !group && a.vec4 && t_rowstride != 0 && Q >= 1 && Q <= 16 && mode != kTile;
+  if (group) {
+    const int R = kMaxBlock / G;
+    a.lds_stride = group_lds_stride(P, G);
+    a.ntiles = (B + R - 1) / R;
+    const size_t lds = (size_t)R * a.lds_stride * sizeof(float);
+    const bool fast = use_fast_math();
+    if (posterior) {
+      if (fast) launch_group_g<true, true>(G, nv_group, a, lds, s, &nblk);
+      else launch_group_g<false, true>(G, nv_group, a, lds, s, &nblk);
+    } else {
+      if (fast) launch_group_g<true, false>(G, nv_group, a, lds, s, &nblk);
+      else launch_group_g<false, false>(G, nv_group, a, lds, s, &nblk);
+    }
+  } else if (persistent) {
     const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;
     a.ownrow = (mode == kOwnRow || !coop_ok) ? 1 : 0;
     a.ntiles = nblk;

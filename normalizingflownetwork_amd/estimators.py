@@ -44,8 +44,8 @@ class _MLP:
         self.weights, self.biases = [], []
         for a, b in zip(sizes[:-1], sizes[1:]):
             lim = float(np.sqrt(6.0 / (a + b)))
-            self.weights.append((torch.rand((a, b), generator=g) * 2 - 1) * lim)
-            self.biases.append(torch.zeros((b,)))
+            self.weights.append((torch.rand((a, b), generator=g, dtype=torch.float32) * 2 - 1) * lim)
+            self.biases.append(torch.zeros((b,), dtype=torch.float32))
         self.activation = activation
         self._device = None
 
@@ -115,8 +115,8 @@ class BaseEstimator:
             self._build(int(x.shape[-1]))
         dev = x.device
         self._mlp.to(dev)
-        xm = torch.as_tensor(self.x_mean, device=dev)
-        xs = torch.as_tensor(self.x_std, device=dev)
+        xm = torch.as_tensor(self.x_mean, dtype=torch.float32, device=dev)
+        xs = torch.as_tensor(self.x_std, dtype=torch.float32, device=dev)
         return self._mlp((x - xm) / (xs + 1e-8)).contiguous()
 
     def __call__(self, x):
@@ -210,8 +210,8 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
         self._mlp.to(dev)
         if self._draw_gen is None:
             self._draw_gen = torch.Generator(device=dev).manual_seed(self.random_seed)
-        xm = torch.as_tensor(self.x_mean, device=dev)
-        xs = torch.as_tensor(self.x_std, device=dev)
+        xm = torch.as_tensor(self.x_mean, dtype=torch.float32, device=dev)
+        xs = torch.as_tensor(self.x_std, dtype=torch.float32, device=dev)
         xn = (x - xm) / (xs + 1e-8)
         act = _ACTIVATIONS[self.activation]
         draws = []
@@ -220,8 +220,10 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
             n = len(self._mlp.weights)
             for i, (w, b) in enumerate(zip(self._mlp.weights, self._mlp.biases)):
                 if not self.map_mode:
-                    w = w + self.posterior_scale * torch.randn(w.shape, generator=self._draw_gen, device=dev)
-                    b = b + self.posterior_scale * torch.randn(b.shape, generator=self._draw_gen, device=dev)
+                    w = w + self.posterior_scale * torch.randn(w.shape, generator=self._draw_gen, device=dev,
+                                                               dtype=torch.float32)
+                    b = b + self.posterior_scale * torch.randn(b.shape, generator=self._draw_gen, device=dev,
+                                                               dtype=torch.float32)
                 h = h @ w + b
                 if i < n - 1:
                     h = act(h)

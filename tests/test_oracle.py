@@ -19,7 +19,7 @@ import torch
 from conftest import CHAIN_FIXTURES, FLOW_FIXTURES, load_golden
 from oracle import nfn_oracle as O
 
-torch.set_default_dtype(torch.float64)
+F64 = torch.float64
 
 
 # ---- independent torch restatement of the forward maps (fp64) -------------------
@@ -53,7 +53,7 @@ T_FWD = {"planar": t_planar, "radial": t_radial, "affine": t_affine}
 
 def autodiff_fldj(ftype, z, tk, d):
     out = []
-    for zi, ti in zip(torch.as_tensor(z), torch.as_tensor(tk)):
+    for zi, ti in zip(torch.as_tensor(z, dtype=F64), torch.as_tensor(tk, dtype=F64)):
         J = torch.func.jacrev(lambda v: T_FWD[ftype](v, ti, d))(zi)
         out.append(torch.linalg.slogdet(J)[1].item())
     return np.array(out)
@@ -67,7 +67,7 @@ def test_fldj_matches_autodiff_jacobian(ftype, d):
     tk = rng.standard_normal((64, ps))
     z = rng.standard_normal((64, d)) * 1.5
     fwd, fldj = O.flow_forward_fldj(ftype, z, tk, d)
-    ref_fwd = np.stack([T_FWD[ftype](torch.as_tensor(zi), torch.as_tensor(ti), d).numpy()
+    ref_fwd = np.stack([T_FWD[ftype](torch.as_tensor(zi, dtype=F64), torch.as_tensor(ti, dtype=F64), d).numpy()
                         for zi, ti in zip(z, tk)])
     np.testing.assert_allclose(fwd, ref_fwd, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(fldj, autodiff_fldj(ftype, z, tk, d), rtol=1e-9, atol=1e-9)
@@ -89,16 +89,16 @@ def test_chain_log_prob_matches_autodiff(d):
         blocks = {}
         for k in reversed(range(len(flows))):
             ps = O.param_size(flows[k], d)
-            blocks[k] = torch.as_tensor(ti[off:off + ps])
+            blocks[k] = torch.as_tensor(ti[off:off + ps], dtype=F64)
             off += ps
-        z = torch.as_tensor(yi)
+        z = torch.as_tensor(yi, dtype=F64)
         ldj = 0.0
         for k, f in enumerate(flows):
             J = torch.func.jacrev(lambda v: T_FWD[f](v, blocks[k], d))(z)
             ldj += torch.linalg.slogdet(J)[1].item()
             z = T_FWD[f](z, blocks[k], d)
-        loc = torch.as_tensor(ti[:d])
-        s = 1e-3 + t_softplus(math.log(math.e - 1) + 0.1 * torch.as_tensor(ti[d:2 * d]))
+        loc = torch.as_tensor(ti[:d], dtype=F64)
+        s = 1e-3 + t_softplus(math.log(math.e - 1) + 0.1 * torch.as_tensor(ti[d:2 * d], dtype=F64))
         base = torch.distributions.Normal(loc, s).log_prob(z).sum().item()
         ref.append(base + ldj)
     np.testing.assert_allclose(lp, np.array(ref), rtol=1e-9, atol=1e-9)

@@ -53,6 +53,7 @@ for s in $STEPS; do
       { cd /tmp; run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o w -- \
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
+    debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
     *) echo "unknown step $s" ;;
   esac
 done
