@@ -101,8 +101,10 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *   out_logp   : (B,) may be NULL when only the sum is wanted
  *   out_sum    : device double[1] or NULL — receives sum_b out_logp[b] (fp64 accumulation)
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
- *                With out_sum == NULL and workspace != NULL only the per-workgroup
- *                partial sums are written (finish with nfn_reduce_sum_f64).
+ *                Layout: workspace[0] = number n of partial sums written,
+ *                workspace[1 .. n] = per-workgroup fp64 partial sums.  With
+ *                out_sum == NULL and workspace != NULL only the partials are written
+ *                (finish with nfn_reduce_partials_f64).
  */
 int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
                               int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
@@ -121,10 +123,17 @@ int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride,
                              void* stream);
 
 /* out[0] = sum of the n doubles at `in` (device), one workgroup, fixed order
- * (deterministic).  Finishes a partials-only chain / posterior call. */
+ * (deterministic). */
 int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream);
 
-/* Number of doubles of device workspace nfn_posterior_lse_f32 needs when out_sum != NULL. */
+/* out[0] = sum of the partials a chain / posterior call left in `workspace`
+ * (workspace[0] = count, workspace[1..count]); finishes a partials-only call. */
+int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream);
+
+/* Number of doubles of device workspace for nfn_posterior_lse_f32: the partials
+ * block (as for the chain) followed by the draw-split region.  Passing a
+ * workspace is optional without out_sum, but enables the draw split (more
+ * parallelism when B is small relative to the GPU). */
 int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P);
 
 /*

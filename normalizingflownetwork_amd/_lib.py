@@ -23,6 +23,7 @@ SIGNATURES = {
     "nfn_last_error": (ctypes.c_char_p, []),
     "nfn_set_math_mode": (_c_int32, [_c_int32]),
     "nfn_reduce_sum_f64": (_c_int32, [_vp, _c_int64, _vp, _vp]),
+    "nfn_reduce_partials_f64": (_c_int32, [_vp, _vp, _vp]),
     "nfn_param_size": (_c_int32, [_c_int32, _c_int32]),
     "nfn_total_param_size": (_c_int32, [_vp, _c_int32, _c_int32, _c_int32]),
     "nfn_chain_workspace_doubles": (_c_int64, [_c_int64, _c_int32, _c_int32]),

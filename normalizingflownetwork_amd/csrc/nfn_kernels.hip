@@ -45,6 +45,19 @@ constexpr float kHalfLog2Pi = 0.91893853320467274f;   // 0.5*log(2*pi)
 constexpr float kLn2 = 0.69314718055994531f;
 constexpr float kLog2e = 1.44269504088896341f;
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte load of a parameter-row piece; NT = non-temporal (streamed once).
+template <bool NT>
+__device__ __forceinline__ float4 load_row4(const float* p) {
+  if constexpr (NT) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+
 struct FlowProgram {
   int32_t K;
   int32_t step[NFN_MAX_FLOWS];  // (param offset << 2) | flow id, application order
@@ -69,6 +82,10 @@ struct ChainArgs {
   int32_t vec4;        // tile rows can be streamed as float4
   int32_t ownrow;      // persistent kernel: each lane streams its own row (else cooperative)
   int64_t ntiles;      // persistent kernel: number of `blockDim.x`-row tiles
+  int32_t nt;          // non-temporal parameter-row loads
+  int32_t nsplit;      // posterior: draw ranges per tile (1 = no split)
+  int32_t dps;         // posterior: draws per range
+  float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   FlowProgram prog;
 };
 
@@ -392,7 +409,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
   }
   if (a.partials) {
     const double s = block_sum(tid < nr ? (double)lp : 0.0, red);
-    if (tid == 0) a.partials[blockIdx.x] = s;
+    if (tid == 0) {
+      a.partials[blockIdx.x] = s;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
   }
 }
 
@@ -441,7 +461,10 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
   }
   if (a.partials) {
     const double s = block_sum(tid < nr ? (double)res : 0.0, red);
-    if (tid == 0) a.partials[blockIdx.x] = s;
+    if (tid == 0) {
+      a.partials[blockIdx.x] = s;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
   }
 }
 
@@ -472,43 +495,68 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
   const int64_t gstep = own ? 4 : (int64_t)rstep * rs;
   const int l0 = r0 * S + 4 * c4;
   const int lstep = own ? 4 : rstep * S;
-  const int ndraw = POST ? a.S : 1;
+  // Work units: (tile, draw range).  The plain chain has one draw and one range;
+  // the posterior may split its S draws into `nsplit` ranges of `dps` draws
+  // (merged by posterior_merge_kernel) to expose more parallelism than B allows.
+  const int nsp = POST ? a.nsplit : 1;
+  const int dps = POST ? a.dps : 1;
+  const int64_t nunits = a.ntiles * nsp;
 
   float4 buf[NV];
   float ybuf[DM];
-  auto issue = [&](int64_t tile, int s) {
+  auto issue = [&](int64_t unit, int s, bool first) {
+    const int64_t tile = POST ? unit / nsp : unit;
     const int64_t b0 = tile * T;
     const int nr = (int)min((int64_t)T, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
+    if (a.nt) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      if (k < Q && r0 + k * rstep < nr) buf[k] = *reinterpret_cast<const float4*>(base + g0 + k * gstep);
+      for (int k = 0; k < NV; ++k) {
+        if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<true>(base + g0 + k * gstep);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<false>(base + g0 + k * gstep);
+      }
     }
-    if (s == 0 && tid < nr) {
+    if (first && tid < nr) {
       const float* yr = a.y + (b0 + tid) * a.y_bstride;
 #pragma unroll
       for (int j = 0; j < DM; ++j) ybuf[j] = (j < a.d) ? yr[j] : 0.0f;
     }
   };
+  auto range_of = [&](int64_t unit, int& sb, int& se) {
+    const int rg = POST ? (int)(unit % nsp) : 0;
+    sb = rg * dps;
+    se = POST ? min(a.S, sb + dps) : 1;
+  };
 
-  // -sum(log y_std) and the normalisation constants are per launch
+  // -sum(log y_std) is per launch
   float corr = 0.0f;
   if (a.y_mean) {
     for (int j = 0; j < a.d; ++j) corr += f_log<FAST>(a.y_std[j]);
   }
 
   double acc = 0.0;
-  // The store of a tile's results is deferred to the next iteration and issued
-  // BEFORE that iteration's prefetch: vmcnt counts stores and loads in issue
-  // order, so a store issued after the prefetch would make the next wait for the
-  // prefetched rows also wait for the store's full latency.
+  // The store of a unit's results is deferred to the next unit and issued BEFORE
+  // that unit's prefetch: vmcnt counts stores and loads in issue order, so a
+  // store issued after the prefetch would make the next wait for the prefetched
+  // rows also wait for the store's full latency.
   int64_t pend_b = -1;
-  float pend_v = 0.0f;
-  int64_t tile = blockIdx.x;
-  if (tile < a.ntiles) issue(tile, 0);
-  for (; tile < a.ntiles; tile += gridDim.x) {
+  float pend_v = 0.0f, pend_m = 0.0f;
+  int64_t unit = blockIdx.x;
+  if (unit < nunits) {
+    int sb, se;
+    range_of(unit, sb, se);
+    issue(unit, sb, true);
+  }
+  for (; unit < nunits; unit += gridDim.x) {
+    const int64_t tile = POST ? unit / nsp : unit;
     const int64_t b0 = tile * T;
     const int nr = (int)min((int64_t)T, a.B - b0);
+    int sb, se;
+    range_of(unit, sb, se);
     float z0[DM];
 #pragma unroll
     for (int j = 0; j < DM; ++j) {
@@ -516,7 +564,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
       if (a.y_mean && j < a.d) z0[j] = f_div<FAST>(z0[j] - a.y_mean[j], a.y_std[j]);
     }
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
-    for (int s = 0; s < ndraw; ++s) {
+    for (int s = sb; s < se; ++s) {
       if (!own) __syncthreads();  // previous unit's LDS rows fully consumed
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
@@ -530,20 +578,28 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
       }
       if (!own) __syncthreads();
       if (pend_b >= 0) {
-        if (a.out) a.out[pend_b] = pend_v;
+        if (!POST || nsp == 1) {
+          if (a.out) a.out[pend_b] = pend_v;
+        } else {
+          a.split_out[pend_b] = make_float2(pend_m, pend_v);
+        }
         pend_b = -1;
       }
-      // prefetch the next unit while this one is evaluated
-      if (s + 1 < ndraw)
-        issue(tile, s + 1);
-      else if (tile + gridDim.x < a.ntiles)
-        issue(tile + gridDim.x, 0);
+      // prefetch the next unit's rows while this one is evaluated
+      if (s + 1 < se) {
+        issue(unit, s + 1, false);
+      } else if (unit + gridDim.x < nunits) {
+        int nb, ne;
+        range_of(unit + gridDim.x, nb, ne);
+        issue(unit + gridDim.x, nb, true);
+      }
       if (tid < nr) {
         float z[DM];
 #pragma unroll
         for (int j = 0; j < DM; ++j) z[j] = z0[j];
         lp = eval_chain<DM, FAST>(z, lds + tid * S, a) - corr;
         if constexpr (POST) {
+          // online logsumexp over draws (scorers.py:25: scipy logsumexp over axis 0)
           if (lp > m) {
             accl = (m == -INFINITY ? 0.0f : accl * f_exp<FAST>(m - lp)) + 1.0f;
             m = lp;
@@ -556,20 +612,76 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
       }
     }
     if (tid < nr) {
-      float res = lp;
-      if constexpr (POST) {
-        res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
-        res = res - f_log<FAST>((float)ndraw);
+      if (POST && nsp > 1) {
+        const int rg = (int)(unit % nsp);
+        pend_b = (int64_t)rg * a.B + b0 + tid;
+        pend_m = m;
+        pend_v = accl;
+      } else {
+        float res = lp;
+        if constexpr (POST) {
+          res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
+          res = res - f_log<FAST>((float)a.S);
+        }
+        pend_b = b0 + tid;
+        pend_v = res;
+        acc += (double)res;
       }
-      pend_b = b0 + tid;
-      pend_v = res;
-      acc += (double)res;
     }
   }
-  if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
-  if (a.partials) {
+  if (pend_b >= 0) {
+    if (!POST || nsp == 1) {
+      if (a.out) a.out[pend_b] = pend_v;
+    } else {
+      a.split_out[pend_b] = make_float2(pend_m, pend_v);
+    }
+  }
+  if (a.partials && (!POST || nsp == 1)) {
     const double sum = block_sum(acc, red);
-    if (tid == 0) a.partials[blockIdx.x] = sum;
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
+
+// Combines the per-range (max, scaled sum) pairs of a draw-split posterior:
+// out[b] = M + log(sum_r acc_r * exp(m_r - M)) - log S, M = max_r m_r.
+template <bool FAST>
+__global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2* __restrict__ parts, int nsplit,
+                                                                     int S, int64_t B, float* __restrict__ out,
+                                                                     double* __restrict__ partials) {
+  __shared__ double red[kMaxBlock / 64];
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float res = 0.0f;
+  if (b < B) {
+    float M = -INFINITY;
+    bool nan = false;
+    for (int r = 0; r < nsplit; ++r) {
+      const float mr = parts[(int64_t)r * B + b].x;
+      nan |= (mr != mr);
+      M = fmaxf(M, mr);
+    }
+    if (nan) {
+      res = NAN;
+    } else if (M == -INFINITY) {
+      res = -INFINITY;
+    } else {
+      float A = 0.0f;
+      for (int r = 0; r < nsplit; ++r) {
+        const float2 pr = parts[(int64_t)r * B + b];
+        if (pr.x > -INFINITY) A += pr.y * f_exp<FAST>(pr.x - M);
+      }
+      res = (M + f_log<FAST>(A)) - f_log<FAST>((float)S);
+    }
+    if (out) out[b] = res;
+  }
+  if (partials) {
+    const double sum = block_sum(b < B ? (double)res : 0.0, red);
+    if (threadIdx.x == 0) {
+      partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
   }
 }
 
@@ -696,9 +808,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
+    if (a.nt) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      if (srow[k] < nr) buf[k] = *reinterpret_cast<const float4*>(base + goff[k]);
+      for (int k = 0; k < NV; ++k) {
+        if (srow[k] < nr) buf[k] = load_row4<true>(base + goff[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (srow[k] < nr) buf[k] = load_row4<false>(base + goff[k]);
+      }
     }
     if (s == 0 && sl < nr && j < a.d) ybuf = a.y[(b0 + sl) * a.y_bstride + j];
   };
@@ -760,7 +879,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
   if (a.partials) {
     const double sum = block_sum(acc, red);
-    if (tid == 0) a.partials[blockIdx.x] = sum;
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
   }
 }
 
@@ -785,6 +907,30 @@ __global__ void __launch_bounds__(kMaxBlock)
       if (j < d) z_out[b * d + j] = z[j];
   }
   if (ldj_out) ldj_out[b] = ldj;
+}
+
+// Sums the partials of a self-describing workspace: ws[0] = count, ws[1..count].
+__global__ void __launch_bounds__(1024) reduce_partials_kernel(const double* __restrict__ ws,
+                                                              double* __restrict__ out) {
+  __shared__ double red[1024 / 64];
+  const int64_t n = (int64_t)ws[0];
+  const double* in = ws + 1;
+  constexpr int U = 8;
+  double acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.0;
+  const int64_t step = (int64_t)blockDim.x * U;
+  int64_t i = threadIdx.x;
+  for (; i + (U - 1) * (int64_t)blockDim.x < n; i += step) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] += in[i + u * (int64_t)blockDim.x];
+  }
+  for (; i < n; i += blockDim.x) acc[0] += in[i];
+  double s = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) s += acc[u];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = s;
 }
 
 __global__ void __launch_bounds__(1024) reduce_f64_kernel(const double* __restrict__ in, int64_t n,
@@ -1013,6 +1159,18 @@ void launch_chain_dm(int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t l
   }
 }
 
+// One fp64 partial per workgroup at the smallest tile (64 rows).
+int64_t partials_capacity(int64_t B) { return (B + 63) / 64; }
+
+// Draw ranges per tile for the posterior: enough (tile, range) units for ~8
+// workgroups per CU on a 256-CU MI355X, at most 16 ranges.
+constexpr int64_t kPosteriorTargetUnits = 2048;
+int posterior_split(int64_t B, int rows) {
+  const int64_t ntiles = (B + rows - 1) / rows;
+  if (ntiles <= 0) return 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (kPosteriorTargetUnits + ntiles - 1) / ntiles));
+}
+
 int32_t check_hip(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(NFN_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -1031,6 +1189,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
   // the flow math, to measure the memory path of the kernel structure alone.
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
+  a.nt = env_int("NFN_NT_LOADS", 0) == 1 ? 1 : 0;  // tuning knob
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
   if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
@@ -1054,7 +1213,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   a.y_mean = y_mean;
   a.y_std = y_std;
   a.out = out;
-  a.partials = workspace;
+  a.partials = workspace ? workspace + 1 : nullptr;  // workspace[0] = number of partials
   a.y_bstride = y_bstride;
   a.t_rowstride = t_rowstride;
   a.t_drawstride = t_drawstride;
@@ -1095,8 +1254,28 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     a.ntiles = nblk;
     const bool fast = use_fast_math();
     if (posterior) {
+      // draw split: more (tile, draw-range) units when the batch alone is too small
+      // to fill the chip; needs the split region of the workspace
+      int nsplit = workspace ? std::min(posterior_split(B, g.rows), S) : 1;
+      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(std::min(env_int("NFN_POST_SPLIT", 1), S),
+                                                             workspace ? posterior_split(B, g.rows) : 1);
+      a.nsplit = nsplit;
+      a.dps = (S + nsplit - 1) / nsplit;
+      a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges
+      a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B));
       if (fast) launch_persistent_dm<true, true>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
       else launch_persistent_dm<false, true>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+      if (a.nsplit > 1) {
+        int32_t rc0 = check_hip("posterior kernel launch");
+        if (rc0 != NFN_OK) return rc0;
+        nblk = (B + kMaxBlock - 1) / kMaxBlock;
+        if (fast)
+          hipLaunchKernelGGL(posterior_merge_kernel<true>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s,
+                             (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1);
+        else
+          hipLaunchKernelGGL(posterior_merge_kernel<false>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s,
+                             (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1);
+      }
     } else {
       if (fast) launch_persistent_dm<true, false>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
       else launch_persistent_dm<false, false>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
@@ -1111,8 +1290,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
   if (rc != NFN_OK) return rc;
   if (out_sum) {
-    hipLaunchKernelGGL(reduce_f64_kernel, dim3(1), dim3(1024), 0, s, (const double*)workspace, nblk, out_sum);
-    rc = check_hip("reduce_f64_kernel launch");
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(1024), 0, s, (const double*)workspace, out_sum);
+    rc = check_hip("reduce_partials_kernel launch");
   }
   return rc;
 }
@@ -1154,11 +1333,21 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   (void)d;
   (void)P;
   if (B <= 0) return 0;
-  return (B + 63) / 64;  // one partial per workgroup at the smallest tile (64 rows)
+  return 1 + partials_capacity(B);  // [count | partials]
 }
 
 int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
-  return nfn_chain_workspace_doubles(B, d, P);
+  if (B <= 0) return 0;
+  // [count | partials | draw-split region: (max, sum) float2 per (range, sample)]
+  return 1 + partials_capacity(B) + (int64_t)posterior_split(B, tile_geom(P < 0 ? 0 : P).rows) * B;
+}
+
+int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream) {
+  g_last_error.clear();
+  if (!workspace || !out) return fail(NFN_E_NULLPTR, "workspace or out is NULL");
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
+                     workspace, out);
+  return check_hip("reduce_partials_kernel launch");
 }
 
 int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B,

@@ -181,7 +181,8 @@ def posterior_lse(
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
     osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
-    ws = _workspace(int(lib.nfn_posterior_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
+    # the workspace also enables the draw split (more parallelism for small B)
+    ws = _workspace(int(lib.nfn_posterior_workspace_doubles(B, n_dims, P)), dev)
     ids, k = flow_ids(flow_types)
     rc = lib.nfn_posterior_lse_f32(
         _ptr(y), _row_stride(y), _ptr(t_draws), int(t_draws.stride(0)), 0 if Bt == 1 else int(t_draws.stride(1)),
@@ -245,7 +246,7 @@ class ChainLauncher:
                 self._trainable, None, None, _ptr(self.out), None, _ptr(self.partials),
             )
             self._fn = self.lib.nfn_chain_logprob_f32
-        self._sum_args = (_ptr(self.partials), self.n_partials, _ptr(self.sum))
+        self._sum_args = (_ptr(self.partials), _ptr(self.sum))
 
     def launch(self, stream: Optional[int] = None) -> None:
         rc = self._fn(*self._args, stream if stream is not None else _stream())
@@ -253,7 +254,7 @@ class ChainLauncher:
             _lib.check(rc, "fused chain launch")
 
     def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
-        rc = self.lib.nfn_reduce_sum_f64(*self._sum_args, stream if stream is not None else _stream())
+        rc = self.lib.nfn_reduce_partials_f64(*self._sum_args, stream if stream is not None else _stream())
         if rc != 0:
-            _lib.check(rc, "nfn_reduce_sum_f64")
+            _lib.check(rc, "nfn_reduce_partials_f64")
         return self.sum

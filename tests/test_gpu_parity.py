@@ -245,9 +245,17 @@ def test_full_size_properties(cfg, gpu):
     lp2, s2 = ops.chain_log_prob(y, t, ft, d, True, want_sum=True)
     # deterministic, bitwise (no atomics, fixed reduction order)
     assert torch.equal(lp1, lp2) and torch.equal(s1, s2)
-    assert torch.isfinite(lp1).all()
+    # non-finite values only where the oracle has them too (a log|det| of 0 is a
+    # legitimate -inf of the reference math)
+    bad = torch.nonzero(~torch.isfinite(lp1)).flatten()
+    assert bad.numel() <= 16
+    if bad.numel():
+        with np.errstate(all="ignore"):
+            r64 = O.chain_log_prob(y[bad].cpu().numpy(), t[bad].cpu().numpy(), ft, d, True, np.float64)
+        np.testing.assert_array_equal(lp1[bad].cpu().numpy(), r64.astype(np.float32))
     # fused fp64 sum == sum of outputs
-    assert float(s1.item()) == pytest.approx(float(lp1.double().sum().item()), rel=1e-12)
+    if bad.numel() == 0:
+        assert float(s1.item()) == pytest.approx(float(lp1.double().sum().item()), rel=1e-12)
     # sum-only launch gives the same sum
     _, s3 = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
     assert torch.equal(s1, s3)
@@ -255,6 +263,10 @@ def test_full_size_properties(cfg, gpu):
     perm = torch.randperm(B, generator=gen, device="cuda")
     lpp, _ = ops.chain_log_prob(y[perm], t[perm], ft, d, True)
     assert torch.equal(lpp, lp1[perm])
+    # the partials-only launch + nfn_reduce_partials_f64 gives the same sum
+    L = ops.ChainLauncher(y, t, ft, d, True, write_values=False)
+    L.launch()
+    assert torch.equal(L.finish_sum(), s1)
     # 4096 random samples (spread over the whole batch) against the oracle
     for what, idx in (("sample", torch.randint(0, B, (4096,), generator=gen, device="cuda")),
                       ("tail", torch.arange(B - 300, B, device="cuda"))):
@@ -281,6 +293,15 @@ def test_full_size_posterior_properties(gpu):
     ref64 = O.posterior_lse(yn, tn, ft, 1, True)
     ref32 = O.posterior_lse(yn, tn, ft, 1, True, dtype=np.float32)
     assert_within(out[idx].cpu().numpy(), ref64, ref32, "C5 sample")
+    # the draw-split path (default at this B) agrees with the single-range path
+    import os
+
+    os.environ["NFN_POST_SPLIT"] = "1"
+    try:
+        out1, _ = ops.posterior_lse(y, t, ft, 1, True)
+    finally:
+        os.environ.pop("NFN_POST_SPLIT")
+    np.testing.assert_allclose(out.cpu().numpy(), out1.cpu().numpy(), rtol=2e-6, atol=2e-6)
     # S copies of one draw: lse - log S == log_prob
     rep = t[:1].expand(S, B, 32).contiguous()
     out_rep, _ = ops.posterior_lse(y, rep, ft, 1, True)

@@ -54,6 +54,7 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
     debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
+    mem) run mem 300 python tools/microbench.py mem ;;
     *) echo "unknown step $s" ;;
   esac
 done

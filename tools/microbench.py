@@ -35,6 +35,7 @@ def run(cfg, variants, reps=20, rounds=3):
     y = torch.randn((B, d), generator=gen, device="cuda")
     t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device="cuda")
     L = ops.ChainLauncher(y, t, ft, d, True, draws=S)
+    L_noout = ops.ChainLauncher(y, t, ft, d, True, write_values=False, draws=S)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     times = {v["name"]: [] for v in variants}
@@ -44,12 +45,13 @@ def run(cfg, variants, reps=20, rounds=3):
             for k, val in v.get("env", {}).items():
                 os.environ[k] = str(val)
             ops.set_math_mode(v.get("math", "fast"))
+            LL = L_noout if v.get("noout") else L
             for _ in range(3):
-                L.launch(sh)
+                LL.launch(sh)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
             for e0, e1 in evs:
                 e0.record(stream)
-                L.launch(sh)
+                LL.launch(sh)
                 e1.record(stream)
             torch.cuda.synchronize()
             times[v["name"]].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
@@ -58,6 +60,8 @@ def run(cfg, variants, reps=20, rounds=3):
             for k in v.get("env", {}):
                 os.environ.pop(k, None)
     ref = outs[variants[0]["name"]]
+    if variants[0].get("noout"):
+        raise SystemExit("first variant must write outputs")
     res = []
     bpl = bytes_per_launch(d, P, B, S)
     for v in variants:
@@ -71,6 +75,22 @@ def run(cfg, variants, reps=20, rounds=3):
 
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "mem":  # memory-path study on C2
+        A = {"NFN_ABLATE_FLOWS": 1}
+        v = [{"name": "auto", "env": {}},
+             {"name": "nt", "env": {"NFN_NT_LOADS": 1}},
+             {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "wg3_nt", "env": {"NFN_WG_PER_CU": 3, "NFN_NT_LOADS": 1}},
+             {"name": "noout", "env": {}, "noout": True},
+             {"name": "ablate", "env": dict(A)},
+             {"name": "ablate_nt", "env": dict(A, NFN_NT_LOADS=1)},
+             {"name": "ablate_noout", "env": dict(A), "noout": True},
+             {"name": "ablate_wg1", "env": dict(A, NFN_WG_PER_CU=1)},
+             {"name": "ablate_wg2", "env": dict(A, NFN_WG_PER_CU=2)},
+             {"name": "ablate_wg3", "env": dict(A, NFN_WG_PER_CU=3)},
+             {"name": "ablate_ownrow_wg2", "env": dict(A, NFN_WG_PER_CU=2, NFN_LOAD_MODE="ownrow")}]
+        run("C2", v)
+        return
     base = [
         {"name": "auto", "env": {}},
         {"name": "coop", "env": {"NFN_LOAD_MODE": "coop"}},
