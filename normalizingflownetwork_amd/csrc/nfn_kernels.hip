@@ -83,6 +83,7 @@ struct ChainArgs {
   int32_t ownrow;      // persistent kernel: each lane streams its own row (else cooperative)
   int64_t ntiles;      // persistent kernel: number of `blockDim.x`-row tiles
   int32_t nt;          // non-temporal parameter-row loads
+  int32_t nt_store;    // non-temporal log_prob stores
   int32_t nsplit;      // posterior: draw ranges per tile (1 = no split)
   int32_t dps;         // posterior: draws per range
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
@@ -478,6 +479,14 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
 //     tid / Q + k * T / Q — each wave instruction reads 1 KiB contiguous;
 //   own-row (ownrow = 1): slot k = float4 k of row tid — each lane streams its
 //     own row, no workgroup barrier is needed at all.
+// Orders this wave's earlier LDS writes before its later LDS reads (and reads
+// before later writes): the wave-tile mode needs no workgroup barrier because a
+// wave only ever reads LDS rows that it wrote itself.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int DM, bool FAST, int NV, bool POST>
 __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a) {
   extern __shared__ float lds[];
@@ -487,10 +496,19 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
   const int Q = a.P >> 2;
   const int S = a.lds_stride;
   const int64_t rs = a.t_rowstride;
-  const bool own = a.ownrow != 0;
-  const int r0 = own ? tid : tid / Q;
-  const int c4 = own ? 0 : tid - (tid / Q) * Q;
-  const int rstep = own ? 0 : T / Q;
+  // Tile teams: the workgroup (cooperative / own-row modes) or each wave on its
+  // own 64-row tile stream (wave mode: no workgroup barriers at all).
+  const int mode = a.ownrow;  // 0 coop, 1 own-row, 2 wave
+  const bool own = mode == 1;
+  const bool wave = mode == 2;
+  const bool wg_sync = mode == 0;
+  const int wid = tid >> 6;
+  const int TR = wave ? 64 : T;          // rows per tile
+  const int lt = wave ? (tid & 63) : tid;  // thread index inside its team
+  float* tl = wave ? lds + wid * 64 * S : lds;
+  const int r0 = own ? lt : lt / Q;
+  const int c4 = own ? 0 : lt - (lt / Q) * Q;
+  const int rstep = own ? 0 : TR / Q;
   const int64_t g0 = (int64_t)r0 * rs + 4 * c4;
   const int64_t gstep = own ? 4 : (int64_t)rstep * rs;
   const int l0 = r0 * S + 4 * c4;
@@ -501,13 +519,29 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
   const int nsp = POST ? a.nsplit : 1;
   const int dps = POST ? a.dps : 1;
   const int64_t nunits = a.ntiles * nsp;
+  const int64_t u0 = wave ? (int64_t)blockIdx.x * (T >> 6) + wid : blockIdx.x;
+  const int64_t ustep = wave ? (int64_t)gridDim.x * (T >> 6) : gridDim.x;
+
+  // y normalisation constants and -sum(log y_std), per launch
+  float ymean[DM], yrstd[DM];
+  float corr = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    ymean[j] = 0.0f;
+    yrstd[j] = 1.0f;
+    if (a.y_mean && j < a.d) {
+      ymean[j] = a.y_mean[j];
+      yrstd[j] = a.y_std[j];
+      corr += f_log<FAST>(yrstd[j]);
+    }
+  }
 
   float4 buf[NV];
   float ybuf[DM];
   auto issue = [&](int64_t unit, int s, bool first) {
     const int64_t tile = POST ? unit / nsp : unit;
-    const int64_t b0 = tile * T;
-    const int nr = (int)min((int64_t)T, a.B - b0);
+    const int64_t b0 = tile * TR;
+    const int nr = (int)min((int64_t)TR, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
     if (a.nt) {
 #pragma unroll
@@ -520,8 +554,8 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
         if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<false>(base + g0 + k * gstep);
       }
     }
-    if (first && tid < nr) {
-      const float* yr = a.y + (b0 + tid) * a.y_bstride;
+    if (first && lt < nr) {
+      const float* yr = a.y + (b0 + lt) * a.y_bstride;
 #pragma unroll
       for (int j = 0; j < DM; ++j) ybuf[j] = (j < a.d) ? yr[j] : 0.0f;
     }
@@ -531,12 +565,14 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
     sb = rg * dps;
     se = POST ? min(a.S, sb + dps) : 1;
   };
-
-  // -sum(log y_std) is per launch
-  float corr = 0.0f;
-  if (a.y_mean) {
-    for (int j = 0; j < a.d; ++j) corr += f_log<FAST>(a.y_std[j]);
-  }
+  auto store_out = [&](int64_t b, float v) {
+    if (a.out) {
+      if (a.nt_store)
+        __builtin_nontemporal_store(v, a.out + b);
+      else
+        a.out[b] = v;
+    }
+  };
 
   double acc = 0.0;
   // The store of a unit's results is deferred to the next unit and issued BEFORE
@@ -545,41 +581,44 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
   // rows also wait for the store's full latency.
   int64_t pend_b = -1;
   float pend_v = 0.0f, pend_m = 0.0f;
-  int64_t unit = blockIdx.x;
+  int64_t unit = u0;
   if (unit < nunits) {
     int sb, se;
     range_of(unit, sb, se);
     issue(unit, sb, true);
   }
-  for (; unit < nunits; unit += gridDim.x) {
+  for (; unit < nunits; unit += ustep) {
     const int64_t tile = POST ? unit / nsp : unit;
-    const int64_t b0 = tile * T;
-    const int nr = (int)min((int64_t)T, a.B - b0);
+    const int64_t b0 = tile * TR;
+    const int nr = (int)min((int64_t)TR, a.B - b0);
     int sb, se;
     range_of(unit, sb, se);
     float z0[DM];
 #pragma unroll
     for (int j = 0; j < DM; ++j) {
       z0[j] = ybuf[j];
-      if (a.y_mean && j < a.d) z0[j] = f_div<FAST>(z0[j] - a.y_mean[j], a.y_std[j]);
+      if (a.y_mean && j < a.d) z0[j] = f_div<FAST>(z0[j] - ymean[j], yrstd[j]);
     }
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = sb; s < se; ++s) {
-      if (!own) __syncthreads();  // previous unit's LDS rows fully consumed
+      if (wg_sync) __syncthreads();  // previous unit's LDS rows fully consumed
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         if (k < Q && r0 + k * rstep < nr) {
-          float* dst = lds + l0 + k * lstep;
+          float* dst = tl + l0 + k * lstep;
           dst[0] = buf[k].x;
           dst[1] = buf[k].y;
           dst[2] = buf[k].z;
           dst[3] = buf[k].w;
         }
       }
-      if (!own) __syncthreads();
+      if (wg_sync)
+        __syncthreads();
+      else if (wave)
+        wave_lds_sync();
       if (pend_b >= 0) {
         if (!POST || nsp == 1) {
-          if (a.out) a.out[pend_b] = pend_v;
+          store_out(pend_b, pend_v);
         } else {
           a.split_out[pend_b] = make_float2(pend_m, pend_v);
         }
@@ -588,16 +627,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
       // prefetch the next unit's rows while this one is evaluated
       if (s + 1 < se) {
         issue(unit, s + 1, false);
-      } else if (unit + gridDim.x < nunits) {
+      } else if (unit + ustep < nunits) {
         int nb, ne;
-        range_of(unit + gridDim.x, nb, ne);
-        issue(unit + gridDim.x, nb, true);
+        range_of(unit + ustep, nb, ne);
+        issue(unit + ustep, nb, true);
       }
-      if (tid < nr) {
+      if (lt < nr) {
         float z[DM];
 #pragma unroll
         for (int j = 0; j < DM; ++j) z[j] = z0[j];
-        lp = eval_chain<DM, FAST>(z, lds + tid * S, a) - corr;
+        lp = eval_chain<DM, FAST>(z, tl + lt * S, a) - corr;
         if constexpr (POST) {
           // online logsumexp over draws (scorers.py:25: scipy logsumexp over axis 0)
           if (lp > m) {
@@ -610,11 +649,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
           }
         }
       }
+      if (wave) wave_lds_sync();  // this tile's LDS reads done before the next writes
     }
-    if (tid < nr) {
+    if (lt < nr) {
       if (POST && nsp > 1) {
         const int rg = (int)(unit % nsp);
-        pend_b = (int64_t)rg * a.B + b0 + tid;
+        pend_b = (int64_t)rg * a.B + b0 + lt;
         pend_m = m;
         pend_v = accl;
       } else {
@@ -623,7 +663,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
           res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
           res = res - f_log<FAST>((float)a.S);
         }
-        pend_b = b0 + tid;
+        pend_b = b0 + lt;
         pend_v = res;
         acc += (double)res;
       }
@@ -631,7 +671,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
   }
   if (pend_b >= 0) {
     if (!POST || nsp == 1) {
-      if (a.out) a.out[pend_b] = pend_v;
+      store_out(pend_b, pend_v);
     } else {
       a.split_out[pend_b] = make_float2(pend_m, pend_v);
     }
@@ -1036,7 +1076,7 @@ int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-enum LoadMode { kAuto = 0, kCoop = 1, kOwnRow = 2, kTile = 3 };
+enum LoadMode { kAuto = 0, kCoop = 1, kOwnRow = 2, kTile = 3, kWave = 4 };
 
 int load_mode_env() {
   const char* e = getenv("NFN_LOAD_MODE");
@@ -1044,6 +1084,7 @@ int load_mode_env() {
   if (!strcmp(e, "coop")) return kCoop;
   if (!strcmp(e, "ownrow")) return kOwnRow;
   if (!strcmp(e, "tile")) return kTile;
+  if (!strcmp(e, "wave")) return kWave;
   return kAuto;
 }
 
@@ -1189,7 +1230,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
   // the flow math, to measure the memory path of the kernel structure alone.
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
-  a.nt = env_int("NFN_NT_LOADS", 0) == 1 ? 1 : 0;  // tuning knob
+  a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
+  a.nt_store = env_int("NFN_NT_STORES", 0) == 1 ? 1 : 0;  // tuning knob
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
   if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
@@ -1249,14 +1291,17 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
       else launch_group_g<false, false>(G, nv_group, a, lds, s, &nblk);
     }
   } else if (persistent) {
-    const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;
-    a.ownrow = (mode == kOwnRow || !coop_ok) ? 1 : 0;
+    const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;  // Q | 64 too (Q <= 16)
+    const bool wave = mode == kWave && coop_ok && g.rows % 64 == 0;
+    a.ownrow = wave ? 2 : ((mode == kOwnRow || !coop_ok) ? 1 : 0);
+    const int tile_rows = wave ? 64 : g.rows;
+    nblk = (B + tile_rows - 1) / tile_rows;
     a.ntiles = nblk;
     const bool fast = use_fast_math();
     if (posterior) {
       // draw split: more (tile, draw-range) units when the batch alone is too small
       // to fill the chip; needs the split region of the workspace
-      int nsplit = workspace ? std::min(posterior_split(B, g.rows), S) : 1;
+      int nsplit = workspace ? std::min(posterior_split(B, tile_rows), S) : 1;
       if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(std::min(env_int("NFN_POST_SPLIT", 1), S),
                                                              workspace ? posterior_split(B, g.rows) : 1);
       a.nsplit = nsplit;

@@ -307,3 +307,26 @@ def test_full_size_posterior_properties(gpu):
     out_rep, _ = ops.posterior_lse(y, rep, ft, 1, True)
     lp, _ = ops.chain_log_prob(y, t[0], ft, 1, True)
     np.testing.assert_allclose(out_rep.cpu().numpy(), lp.cpu().numpy(), rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("mode", ["coop", "wave", "ownrow", "tile"])
+def test_load_modes_bitwise_equal(mode, gpu):
+    """Every tile-streaming strategy evaluates each sample with the same math, so
+    the per-sample outputs are bitwise identical across strategies."""
+    import os
+
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden("stress_pr5_d1")
+    ref, _ = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], 1, True)
+    gp = load_golden("posterior_s8_pr5_d1")
+    pref, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
+    os.environ["NFN_LOAD_MODE"] = mode
+    try:
+        got, s = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], 1, True, want_sum=True)
+        pgot, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
+    finally:
+        os.environ.pop("NFN_LOAD_MODE")
+    assert torch.equal(got, ref)
+    assert float(s.item()) == pytest.approx(float(got.double().sum().item()), rel=1e-12)
+    np.testing.assert_allclose(pgot.cpu().numpy(), pref.cpu().numpy(), rtol=2e-6, atol=2e-6)

@@ -55,6 +55,7 @@ for s in $STEPS; do
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
     debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
     mem) run mem 300 python tools/microbench.py mem ;;
+    mode) run mode 300 python tools/microbench.py mode ;;
     *) echo "unknown step $s" ;;
   esac
 done

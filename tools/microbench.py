@@ -75,6 +75,23 @@ def run(cfg, variants, reps=20, rounds=3):
 
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "mode":  # load-mode study, C2 and C5
+        for cfg in ("C2", "C5"):
+            v = [{"name": "coop", "env": {"NFN_LOAD_MODE": "coop"}},
+                 {"name": "wave", "env": {"NFN_LOAD_MODE": "wave"}},
+                 {"name": "coop_ntst", "env": {"NFN_LOAD_MODE": "coop", "NFN_NT_STORES": 1}},
+                 {"name": "wave_ntst", "env": {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}},
+                 {"name": "coop_wg3", "env": {"NFN_LOAD_MODE": "coop", "NFN_WG_PER_CU": 3}},
+                 {"name": "wave_wg3", "env": {"NFN_LOAD_MODE": "wave", "NFN_WG_PER_CU": 3}},
+                 {"name": "wave_wg2", "env": {"NFN_LOAD_MODE": "wave", "NFN_WG_PER_CU": 2}},
+                 {"name": "coop_nont", "env": {"NFN_LOAD_MODE": "coop", "NFN_NT_LOADS": 0}},
+                 {"name": "wave_ablate", "env": {"NFN_LOAD_MODE": "wave", "NFN_ABLATE_FLOWS": 1}},
+                 {"name": "coop_ablate", "env": {"NFN_LOAD_MODE": "coop", "NFN_ABLATE_FLOWS": 1}}]
+            if cfg == "C5":
+                v += [{"name": "coop_nosplit", "env": {"NFN_LOAD_MODE": "coop", "NFN_POST_SPLIT": 1}},
+                      {"name": "wave_nosplit", "env": {"NFN_LOAD_MODE": "wave", "NFN_POST_SPLIT": 1}}]
+            run(cfg, v)
+        return
     if which[0] == "mem":  # memory-path study on C2
         A = {"NFN_ABLATE_FLOWS": 1}
         v = [{"name": "auto", "env": {}},
