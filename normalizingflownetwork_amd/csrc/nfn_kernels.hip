@@ -84,6 +84,7 @@ struct ChainArgs {
   int64_t ntiles;      // persistent kernel: number of `blockDim.x`-row tiles
   int32_t nt;          // non-temporal parameter-row loads
   int32_t nt_store;    // non-temporal log_prob stores
+  int32_t ablate_loads;  // diagnostic: stream only the first tile (compute-only timing)
   int32_t nsplit;      // posterior: draw ranges per tile (1 = no split)
   int32_t dps;         // posterior: draws per range
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
@@ -538,11 +539,14 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
 
   float4 buf[NV];
   float ybuf[DM];
+  bool issued_once = false;
   auto issue = [&](int64_t unit, int s, bool first) {
     const int64_t tile = POST ? unit / nsp : unit;
     const int64_t b0 = tile * TR;
     const int nr = (int)min((int64_t)TR, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
+    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    issued_once = true;
     if (a.nt) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
@@ -1232,6 +1236,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
   a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
   a.nt_store = env_int("NFN_NT_STORES", 0) == 1 ? 1 : 0;  // tuning knob
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
   if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");

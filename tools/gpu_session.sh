@@ -56,6 +56,7 @@ for s in $STEPS; do
     debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
     mem) run mem 300 python tools/microbench.py mem ;;
     mode) run mode 300 python tools/microbench.py mode ;;
+    valu) run valu 300 python tools/microbench.py valu ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -75,6 +75,16 @@ def run(cfg, variants, reps=20, rounds=3):
 
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "valu":  # compute vs memory floors
+        for cfg in ("C2", "C5"):
+            W = {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}
+            v = [{"name": "wave", "env": dict(W)},
+                 {"name": "compute_only", "env": dict(W, NFN_ABLATE_LOADS=1)},
+                 {"name": "memory_only", "env": dict(W, NFN_ABLATE_FLOWS=1)},
+                 {"name": "precise", "env": dict(W), "math": "precise"},
+                 {"name": "precise_compute_only", "env": dict(W, NFN_ABLATE_LOADS=1), "math": "precise"}]
+            run(cfg, v)
+        return
     if which[0] == "mode":  # load-mode study, C2 and C5
         for cfg in ("C2", "C5"):
             v = [{"name": "coop", "env": {"NFN_LOAD_MODE": "coop"}},
