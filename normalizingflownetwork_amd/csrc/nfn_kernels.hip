@@ -60,6 +60,7 @@ __device__ __forceinline__ float4 load_row4(const float* p) {
 
 struct FlowProgram {
   int32_t K;
+  uint32_t types;               // K <= 16: flow ids, 2 bits each, application order
   int32_t step[NFN_MAX_FLOWS];  // (param offset << 2) | flow id, application order
 };
 
@@ -327,6 +328,146 @@ __device__ __forceinline__ float eval_chain(float (&z)[DM], const float* row, co
   return base_log_prob<DM, FAST>(z, row, d, a.trainable != 0) + ildj;
 }
 
+// ---------------------------------------------------------------------------
+// d = 1 fast path (configs C1, C2, C5).  Every flow has <= 3 parameters at d = 1,
+// so the chain is software-pipelined: while flow k is evaluated, flow k+1's
+// step word (scalar load) and its three parameters (LDS reads) are already in
+// flight.  Log-determinants are accumulated in log2 and scaled by ln 2 once, and
+// softplus uses log2(1 + e) directly (absolute error ~1 ulp of 1, which is what
+// every softplus consumer here — -1 + softplus + 1e-5, alpha, beta, the base
+// scale — is sensitive to).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sp_fast1(float x) {
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+  const float sp = fmaxf(x, 0.0f) + __builtin_amdgcn_logf(1.0f + e) * kLn2;
+  return x > kSoftplusThr ? x : sp;
+}
+
+// returns log2|det|
+__device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, float b) {
+  const float w = wraw + 1.0f;
+  const float wtu = w * u;
+  const float nw2 = w * w + 1e-9f;
+  const float m_wtu = (-1.0f + sp_fast1(wtu)) + 1e-5f;
+  const float coef = m_wtu - wtu;
+  const float uh = u + coef * f_div_acc<true>(w, nw2);
+  const float th = f_tanh<true>(w * z + b);
+  z = z + uh * th;
+  const float dth = 1.0f - th * th;
+  return __builtin_amdgcn_logf(fabsf(1.0f + uh * (dth * w)));
+}
+
+__device__ __forceinline__ float radial1_fast(float& z, float a0, float b0, float g) {
+  const float alpha = sp_fast1(0.3f * a0 - 2.0f);
+  const float beta = sp_fast1(0.1f * b0 + kLogExpm1One) - 1.0f;
+  const float r = fabsf(z - g);
+  const float h = __builtin_amdgcn_rcpf(alpha + r);
+  const float ab = alpha * beta;
+  const float abh = ab * h;
+  z = z + abh * (z - g);
+  const float A = 1.0f + abh;
+  return __builtin_amdgcn_logf(A + (ab * (-h * h)) * r);  // (1+abh)^0 * (...)
+}
+
+__device__ __forceinline__ float affine1_fast(float& z, float sh, float scraw) {
+  const float sc = 1.0f + scraw;
+  z = z * sc + sh;
+  return __builtin_amdgcn_logf(fabsf(sc));
+}
+
+__device__ __forceinline__ void read3(float (&v)[3], const float* row, int st) {
+  const float* p = row + (st >> 2);
+  v[0] = p[0];
+  v[1] = p[1];
+  v[2] = (st & 3) == NFN_FLOW_AFFINE ? 0.0f : p[2];
+}
+
+// Chains of up to 16 flows: the flow types are packed 2 bits per flow in one
+// 32-bit kernel argument and every block offset is derived with scalar
+// arithmetic (blocks are stored in reverse application order, so
+// off_0 = P - size(f_0) and off_{k+1} = off_k - size(f_{k+1})).  The unrolled
+// chain body then holds no memory access for the program at all — only in-order
+// LDS parameter reads, which for flow k+1 are issued before flow k's math.
+__device__ __forceinline__ int size1(int id) { return id == NFN_FLOW_AFFINE ? 2 : 3; }
+
+__device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, uint32_t types, int K, int P) {
+  float l2 = 0.0f;
+  int id = (int)(types & 3u);
+  int off = P - size1(id);
+  // Parameter reads are unconditional (3 floats, offset clamped at 0; the LDS
+  // tile is padded) so that no control flow separates a read from its use and
+  // the waitcnt pass can count the in-order LDS returns instead of draining.
+  float pc[3];
+  pc[0] = row[off];
+  pc[1] = row[off + 1];
+  pc[2] = row[off + 2];
+#pragma unroll 1
+  for (int k = 0; k < 16; ++k) {
+    if (k < K) {
+      const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
+      const int offn = max(off - size1(idn), 0);
+      float pn[3];
+      pn[0] = row[offn];
+      pn[1] = row[offn + 1];
+      pn[2] = row[offn + 2];
+      float l;
+      if (id == NFN_FLOW_PLANAR)
+        l = planar1_fast(z, pc[0], pc[1], pc[2]);
+      else if (id == NFN_FLOW_RADIAL)
+        l = radial1_fast(z, pc[0], pc[1], pc[2]);
+      else
+        l = affine1_fast(z, pc[0], pc[1]);
+      l2 += l;
+      id = idn;
+      off = offn;
+      pc[0] = pn[0];
+      pc[1] = pn[1];
+      pc[2] = pn[2];
+    }
+  }
+  return l2;
+}
+
+template <bool PACKED>
+__device__ __forceinline__ float eval_chain1_fast(float z, const float* row, const ChainArgs& a) {
+  const int K = a.prog.K;
+  float l2 = 0.0f;  // sum of log2|det J_k|
+  if constexpr (PACKED) {
+    if (K > 0) l2 = chain1_fast_packed(z, row, a.prog.types, K, a.P);
+  } else if (K > 0) {
+    int st = a.prog.step[0];
+    float pc[3];
+    read3(pc, row, st);
+    for (int k = 0; k < K; ++k) {
+      const int stn = (k + 1 < K) ? a.prog.step[k + 1] : 0;
+      float pn[3];
+      if (k + 1 < K) read3(pn, row, stn);
+      const int id = st & 3;
+      float l;
+      if (id == NFN_FLOW_PLANAR)
+        l = planar1_fast(z, pc[0], pc[1], pc[2]);
+      else if (id == NFN_FLOW_RADIAL)
+        l = radial1_fast(z, pc[0], pc[1], pc[2]);
+      else
+        l = affine1_fast(z, pc[0], pc[1]);
+      l2 += l;
+      st = stn;
+      pc[0] = pn[0];
+      pc[1] = pn[1];
+      pc[2] = pn[2];
+    }
+  }
+  float base;
+  if (a.trainable) {
+    const float sc = 1e-3f + sp_fast1(kLogExpm1One + 0.1f * row[1]);
+    const float zz = f_div<true>(z - row[0], sc);
+    base = -0.5f * (zz * zz) - (kHalfLog2Pi + __builtin_amdgcn_logf(sc) * kLn2);
+  } else {
+    base = -0.5f * (z * z) - kHalfLog2Pi;
+  }
+  return base + l2 * kLn2;
+}
+
 // Stream `nr` parameter rows of width P (global row stride rs) into LDS rows of
 // stride S.  Coalesced: consecutive lanes take consecutive 16-byte (or 4-byte)
 // pieces of the contiguous row block.
@@ -488,8 +629,8 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int DM, bool FAST, int NV, bool POST>
-__global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a) {
+template <int DM, bool FAST, int NV, bool POST, bool PACKED>
+__global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
   const int T = blockDim.x;
@@ -640,7 +781,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_persistent_kernel(ChainArgs a
         float z[DM];
 #pragma unroll
         for (int j = 0; j < DM; ++j) z[j] = z0[j];
-        lp = eval_chain<DM, FAST>(z, tl + lt * S, a) - corr;
+        if constexpr (DM == 1 && FAST)
+          lp = eval_chain1_fast<PACKED>(z[0], tl + lt * S, a) - corr;
+        else
+          lp = eval_chain<DM, FAST>(z, tl + lt * S, a) - corr;
         if constexpr (POST) {
           // online logsumexp over draws (scorers.py:25: scipy logsumexp over axis 0)
           if (lp > m) {
@@ -1039,7 +1183,11 @@ int32_t build_program(const int32_t* flow_ids, int32_t K, int32_t d, int32_t tra
     if (prog) prog->step[k] = (off << 2) | flow_ids[k];
     off += ps;
   }
-  if (prog) prog->K = K;
+  if (prog) {
+    prog->K = K;
+    prog->types = 0;
+    for (int32_t k = 0; k < K && k < 16; ++k) prog->types |= (uint32_t)flow_ids[k] << (2 * k);
+  }
   return off;
 }
 
@@ -1102,7 +1250,10 @@ int cu_count() {
 template <int DM, bool FAST, int NV, bool POST>
 void launch_persistent(const ChainArgs& a0, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
   ChainArgs a = a0;
-  auto kfn = chain_persistent_kernel<DM, FAST, NV, POST>;
+  // the packed-program fast path exists for d = 1 chains of <= 16 flows
+  auto kfn = (DM == 1 && FAST && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
+                 ? chain_persistent_kernel<DM, FAST, NV, POST, DM == 1 && FAST>
+                 : chain_persistent_kernel<DM, FAST, NV, POST, false>;
   int occ = env_int("NFN_WG_PER_CU", 0);
   if (occ <= 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, T, lds) != hipSuccess || occ <= 0) occ = 1;
@@ -1300,6 +1451,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     const bool wave = mode == kWave && coop_ok && g.rows % 64 == 0;
     a.ownrow = wave ? 2 : ((mode == kOwnRow || !coop_ok) ? 1 : 0);
     const int tile_rows = wave ? 64 : g.rows;
+    const size_t lds_p = g.lds_bytes + 16;  // the packed d = 1 chain may read 3 floats past a row
     nblk = (B + tile_rows - 1) / tile_rows;
     a.ntiles = nblk;
     const bool fast = use_fast_math();
@@ -1313,8 +1465,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
       a.dps = (S + nsplit - 1) / nsplit;
       a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges
       a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B));
-      if (fast) launch_persistent_dm<true, true>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
-      else launch_persistent_dm<false, true>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+      if (fast) launch_persistent_dm<true, true>(dm, Q, a, g.rows, lds_p, s, &nblk);
+      else launch_persistent_dm<false, true>(dm, Q, a, g.rows, lds_p, s, &nblk);
       if (a.nsplit > 1) {
         int32_t rc0 = check_hip("posterior kernel launch");
         if (rc0 != NFN_OK) return rc0;
@@ -1327,8 +1479,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
                              (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1);
       }
     } else {
-      if (fast) launch_persistent_dm<true, false>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
-      else launch_persistent_dm<false, false>(dm, Q, a, g.rows, g.lds_bytes, s, &nblk);
+      if (fast) launch_persistent_dm<true, false>(dm, Q, a, g.rows, lds_p, s, &nblk);
+      else launch_persistent_dm<false, false>(dm, Q, a, g.rows, lds_p, s, &nblk);
     }
   } else {
     const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
