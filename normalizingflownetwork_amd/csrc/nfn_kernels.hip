@@ -468,6 +468,16 @@ __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, con
   return base + l2 * kLn2;
 }
 
+// One evaluator per (DM, FAST) for every kernel, so all tile-streaming strategies
+// produce bitwise-identical per-sample results.
+template <int DM, bool FAST>
+__device__ __forceinline__ float eval_sample(float (&z)[DM], const float* row, const ChainArgs& a) {
+  if constexpr (DM == 1 && FAST)
+    return eval_chain1_fast<false>(z[0], row, a);
+  else
+    return eval_chain<DM, FAST>(z, row, a);
+}
+
 // Stream `nr` parameter rows of width P (global row stride rs) into LDS rows of
 // stride S.  Coalesced: consecutive lanes take consecutive 16-byte (or 4-byte)
 // pieces of the contiguous row block.
@@ -547,7 +557,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
     float z[DM];
     const int64_t b = b0 + tid;
     const float corr = load_y<DM, FAST>(z, a, b);
-    lp = eval_chain<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
+    lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
     if (a.out) a.out[b] = lp;
   }
   if (a.partials) {
@@ -584,7 +594,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
       float z[DM];
 #pragma unroll
       for (int j = 0; j < DM; ++j) z[j] = y0[j];
-      const float lp = eval_chain<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
+      const float lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
       // online logsumexp (scorers.py:25 uses scipy.special.logsumexp over axis 0)
       if (lp > m) {
         acc = (m == -INFINITY ? 0.0f : acc * f_exp<FAST>(m - lp)) + 1.0f;
@@ -885,10 +895,22 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2
 // are accumulated per lane and reduced once at the end.
 // ---------------------------------------------------------------------------
 
+// Butterfly sum inside G-lane groups with DPP (one VALU op per step, no LDS):
+// quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), row_half_mirror
+// (8-lane combine), row_mirror (16-lane combine); xor 16 via a lane shuffle.
+// Every lane of a group ends with the bitwise-identical sum (fp add commutes).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
 template <int G>
 __device__ __forceinline__ float gsum(float v) {
-#pragma unroll
-  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, G);
+  if constexpr (G >= 2) v += dpp_mov<0xB1>(v);
+  if constexpr (G >= 4) v += dpp_mov<0x4E>(v);
+  if constexpr (G >= 8) v += dpp_mov<0x141>(v);
+  if constexpr (G >= 16) v += dpp_mov<0x140>(v);
+  if constexpr (G >= 32) v += __shfl_xor(v, 16, 32);
   return v;
 }
 
@@ -937,7 +959,130 @@ __device__ __forceinline__ float radial_step_g(float& z, const float* p, int d, 
 }
 
 template <int G, bool FAST>
+__device__ __forceinline__ float eval_chain_g_rolled(float z, const float* row, const ChainArgs& a, int j);
+
+// Register-parameter forms of the group steps (parameters read ahead of time).
+template <int G, bool FAST>
+__device__ __forceinline__ float planar_g_regs(float& z, float u, float wraw, float b, bool act) {
+  const float w = act ? wraw + 1.0f : 0.0f;
+  u = act ? u : 0.0f;
+  const float wtu = gsum<G>(w * u);
+  const float nw2 = gsum<G>(w * w);
+  const float wz = gsum<G>(w * z);
+  const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
+  const float norm_w2 = nw2 + 1e-9f;
+  const float coef = m_wtu - wtu;
+  const float th = f_tanh<FAST>(wz + b);
+  const float dth = 1.0f - th * th;
+  const float uh = u + coef * f_div_acc<FAST>(w, norm_w2);  // 0 on inactive lanes
+  z = z + uh * th;
+  const float sdet = gsum<G>(uh * (dth * w));
+  return f_log<FAST>(fabsf(1.0f + sdet));
+}
+
+template <int G, bool FAST>
+__device__ __forceinline__ float radial_g_regs(float& z, float a0, float b0, float g, int d, bool act) {
+  const float alpha = softplus_tf<FAST>(0.3f * a0 - 2.0f);
+  const float beta = softplus_tf<FAST>(0.1f * b0 + kLogExpm1One) - 1.0f;
+  const float r = gsum<G>(act ? fabsf(z - g) : 0.0f);
+  const float yv = alpha + r;
+  float h, der_h;
+  if constexpr (FAST) {
+    h = __builtin_amdgcn_rcpf(yv);
+    der_h = -h * h;
+  } else {
+    h = 1.0f / yv;
+    der_h = (-1.0f / yv) / yv;
+  }
+  const float ab = alpha * beta;
+  const float abh = ab * h;
+  if (act) z = z + abh * (z - g);
+  const float A = 1.0f + abh;
+  const float Bv = A + (ab * der_h) * r;
+  float Ap = 1.0f;
+  for (int i = 1; i < d; ++i) Ap *= A;
+  return f_log<FAST>(Ap * Bv);
+}
+
+// Chains of <= 16 flows: packed flow types, scalar offsets, and the next flow's
+// three per-lane parameters read while the current flow is evaluated.
+//   planar: (u_j, w'_j, b) at (j, d+j, 2d); radial: (a, b, gamma_j) at (0, 1, 2+j);
+//   affine: (shift_j, scale'_j) at (j, d+j).
+template <int G, bool FAST>
+__device__ __forceinline__ float chain_g_packed(float& z, float& dimterm, const float* row, const ChainArgs& a,
+                                                int j) {
+  const int d = a.d;
+  const int K = a.prog.K;
+  const uint32_t types = a.prog.types;
+  const bool act = j < d;
+  auto size_of = [&](int id) { return id == NFN_FLOW_PLANAR ? 2 * d + 1 : (id == NFN_FLOW_RADIAL ? d + 2 : 2 * d); };
+  auto read = [&](int id, int off, float& x1, float& x2, float& x3) {
+    const float* p = row + off;
+    if (id == NFN_FLOW_RADIAL) {
+      x1 = p[0];
+      x2 = p[1];
+      x3 = p[2 + j];
+    } else {
+      x1 = p[j];
+      x2 = p[d + j];
+      x3 = p[2 * d];
+    }
+  };
+  float ildj = 0.0f;
+  int id = (int)(types & 3u);
+  int off = a.P - size_of(id);
+  float c1, c2, c3;
+  read(id, off, c1, c2, c3);
+#pragma unroll 1
+  for (int k = 0; k < 16; ++k) {
+    if (k < K) {
+      const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
+      const int offn = max(off - size_of(idn), 0);
+      float n1, n2, n3;
+      read(idn, offn, n1, n2, n3);
+      if (id == NFN_FLOW_PLANAR) {
+        ildj = ildj + planar_g_regs<G, FAST>(z, c1, c2, c3, act);
+      } else if (id == NFN_FLOW_RADIAL) {
+        ildj = ildj + radial_g_regs<G, FAST>(z, c1, c2, c3, d, act);
+      } else if (act) {
+        const float sc = 1.0f + c2;
+        z = z * sc + c1;
+        dimterm += f_log<FAST>(fabsf(sc));
+      }
+      id = idn;
+      off = offn;
+      c1 = n1;
+      c2 = n2;
+      c3 = n3;
+    }
+  }
+  return ildj;
+}
+
+template <int G, bool FAST, bool PACKED>
 __device__ __forceinline__ float eval_chain_g(float z, const float* row, const ChainArgs& a, int j) {
+  if constexpr (PACKED) {
+    const int d = a.d;
+    const bool act = j < d;
+    float dimterm = 0.0f;
+    const float ildj = a.prog.K > 0 ? chain_g_packed<G, FAST>(z, dimterm, row, a, j) : 0.0f;
+    if (act) {
+      if (a.trainable) {
+        const float sc = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + j]);
+        const float zz = f_div<FAST>(z - row[j], sc);
+        dimterm += -0.5f * (zz * zz) - f_log<FAST>(sc);
+      } else {
+        dimterm += -0.5f * (z * z);
+      }
+    }
+    return (gsum<G>(dimterm) - kHalfLog2Pi * (float)d) + ildj;
+  } else {
+    return eval_chain_g_rolled<G, FAST>(z, row, a, j);
+  }
+}
+
+template <int G, bool FAST>
+__device__ __forceinline__ float eval_chain_g_rolled(float z, const float* row, const ChainArgs& a, int j) {
   const int d = a.d;
   const bool act = j < d;
   float ildj = 0.0f, dimterm = 0.0f;
@@ -967,7 +1112,7 @@ __device__ __forceinline__ float eval_chain_g(float z, const float* row, const C
   return (gsum<G>(dimterm) - kHalfLog2Pi * (float)d) + ildj;
 }
 
-template <int G, bool FAST, int NV, bool POST>
+template <int G, bool FAST, int NV, bool POST, bool PACKED>
 __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
@@ -992,10 +1137,13 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   }
   float4 buf[NV];
   float ybuf = 0.0f;
+  bool issued_once = false;
   auto issue = [&](int64_t tile, int s) {
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
+    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    issued_once = true;
     if (a.nt) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
@@ -1032,7 +1180,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
       }
       __syncthreads();
       if (pend_b >= 0) {
-        if (a.out) a.out[pend_b] = pend_v;
+        if (a.out) {
+          if (a.nt_store)
+            __builtin_nontemporal_store(pend_v, a.out + pend_b);
+          else
+            a.out[pend_b] = pend_v;
+        }
         pend_b = -1;
       }
       if (s + 1 < ndraw)
@@ -1040,7 +1193,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
       else if (tile + gridDim.x < a.ntiles)
         issue(tile + gridDim.x, 0);
       if (sl < nr) {
-        lp = eval_chain_g<G, FAST>(z0, lds + sl * S, a, j) - corr;
+        lp = eval_chain_g<G, FAST, PACKED>(z0, lds + sl * S, a, j) - corr;
         if constexpr (POST) {
           if (lp > m) {
             accl = (m == -INFINITY ? 0.0f : accl * f_exp<FAST>(m - lp)) + 1.0f;
@@ -1301,7 +1454,8 @@ int group_lds_stride(int P, int G) {
 template <int G, bool FAST, int NV, bool POST>
 void launch_group(const ChainArgs& a0, size_t lds, hipStream_t s, int64_t* grid_out) {
   ChainArgs a = a0;
-  auto kfn = chain_group_kernel<G, FAST, NV, POST>;
+  auto kfn = (a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? chain_group_kernel<G, FAST, NV, POST, true>
+                                                                : chain_group_kernel<G, FAST, NV, POST, false>;
   int occ = env_int("NFN_WG_PER_CU", 0);
   if (occ <= 0) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, kMaxBlock, lds) != hipSuccess || occ <= 0) occ = 1;
@@ -1386,7 +1540,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   // the flow math, to measure the memory path of the kernel structure alone.
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
   a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
-  a.nt_store = env_int("NFN_NT_STORES", 0) == 1 ? 1 : 0;  // tuning knob
+  a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
@@ -1437,7 +1591,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     const int R = kMaxBlock / G;
     a.lds_stride = group_lds_stride(P, G);
     a.ntiles = (B + R - 1) / R;
-    const size_t lds = (size_t)R * a.lds_stride * sizeof(float);
+    const size_t lds = (size_t)R * a.lds_stride * sizeof(float) + (G + 4) * sizeof(float);  // + read-ahead pad
     const bool fast = use_fast_math();
     if (posterior) {
       if (fast) launch_group_g<true, true>(G, nv_group, a, lds, s, &nblk);
@@ -1448,7 +1602,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     }
   } else if (persistent) {
     const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;  // Q | 64 too (Q <= 16)
-    const bool wave = mode == kWave && coop_ok && g.rows % 64 == 0;
+    // default: wave-tile streaming (measured fastest on C2/C5); coop / ownrow on request
+    const bool wave = (mode == kWave || mode == kAuto) && coop_ok && g.rows % 64 == 0;
     a.ownrow = wave ? 2 : ((mode == kOwnRow || !coop_ok) ? 1 : 0);
     const int tile_rows = wave ? 64 : g.rows;
     const size_t lds_p = g.lds_bytes + 16;  // the packed d = 1 chain may read 3 floats past a row

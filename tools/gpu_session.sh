@@ -57,6 +57,7 @@ for s in $STEPS; do
     mem) run mem 300 python tools/microbench.py mem ;;
     mode) run mode 300 python tools/microbench.py mode ;;
     valu) run valu 300 python tools/microbench.py valu ;;
+    c3micro) run c3micro 300 python tools/microbench.py c3 ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -75,6 +75,17 @@ def run(cfg, variants, reps=20, rounds=3):
 
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "c3":  # wide-event group kernel
+        v = [{"name": "auto", "env": {}},
+             {"name": "rolled", "env": {"NFN_PACKED": 0}},
+             {"name": "tile", "env": {"NFN_LOAD_MODE": "tile"}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "wg4", "env": {"NFN_WG_PER_CU": 4}},
+             {"name": "wg6", "env": {"NFN_WG_PER_CU": 6}},
+             {"name": "wg8", "env": {"NFN_WG_PER_CU": 8}}]
+        run("C3", v)
+        return
     if which[0] == "valu":  # compute vs memory floors
         for cfg in ("C2", "C5"):
             W = {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}
