@@ -1,4 +1,8 @@
-"""Build ``libnfn_hip.so`` in-tree for gfx950 (``python -m normalizingflownetwork_amd.build``)."""
+"""Build ``libnfn_hip.so`` in-tree for gfx950 (``python -m normalizingflownetwork_amd.build``).
+
+The kernels are split over several translation units (fast / precise math
+instantiations compile as separate objects) that are compiled in parallel and
+linked into one shared library."""
 
 from __future__ import annotations
 
@@ -6,12 +10,27 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-SRC = os.path.join(PKG_DIR, "csrc", "nfn_kernels.hip")
+CSRC = os.path.join(PKG_DIR, "csrc")
+OBJ_DIR = os.path.join(PKG_DIR, "_obj")
 OUT = os.path.join(PKG_DIR, "libnfn_hip.so")
 ARCH = os.environ.get("NFN_OFFLOAD_ARCH", "gfx950")
+HEADERS = [os.path.join(CSRC, "nfn_device.h"), os.path.join(CSRC, "nfn_launch.h"),
+           os.path.join(REPO_DIR, "include", "nfn.h")]
+# (object name, source, extra flags)
+UNITS = [
+    ("api", "nfn_api.hip", []),
+    ("persistent_fast", "nfn_persistent.hip", ["-DNFN_FAST=1"]),
+    ("persistent_precise", "nfn_persistent.hip", ["-DNFN_FAST=0"]),
+    ("group_fast", "nfn_group.hip", ["-DNFN_FAST=1"]),
+    ("group_precise", "nfn_group.hip", ["-DNFN_FAST=0"]),
+    ("tile", "nfn_tile.hip", []),
+    ("misc", "nfn_misc.hip", []),
+]
+SOURCES = sorted({os.path.join(CSRC, u[1]) for u in UNITS})
 
 
 def hipcc() -> str:
@@ -21,33 +40,47 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def command(out: str = OUT) -> list:
-    return [
-        hipcc(),
-        f"--offload-arch={ARCH}",
-        "-O3",
-        "-std=c++17",
-        "-fPIC",
-        "-shared",
-        "-Wall",
-        "-I",
-        os.path.join(REPO_DIR, "include"),
-        "-o",
-        out,
-        SRC,
-    ]
+def _common() -> list:
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(REPO_DIR, "include")]
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    """Compile the HIP library unless it is newer than its sources."""
-    deps = [SRC, os.path.join(REPO_DIR, "include", "nfn.h")]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(p) for p in deps):
-        return OUT
-    cmd = command(OUT + ".tmp")
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(unit, verbose: bool) -> str:
+    name, src, flags = unit
+    obj = os.path.join(OBJ_DIR, name + ".o")
+    srcp = os.path.join(CSRC, src)
+    if _stale(obj, [srcp] + HEADERS):
+        cmd = [hipcc()] + _common() + flags + ["-c", srcp, "-o", obj + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
+    """Compile (in parallel) the translation units that are out of date and link."""
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    if force:
+        for u in UNITS:
+            p = os.path.join(OBJ_DIR, u[0] + ".o")
+            if os.path.exists(p):
+                os.remove(p)
+    jobs = jobs or min(len(UNITS), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda u: _compile(u, verbose), UNITS))
+    if force or _stale(OUT, objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
     return OUT
 
 

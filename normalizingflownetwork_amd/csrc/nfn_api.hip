@@ -1,0 +1,354 @@
+// nfn_api.hip — the extern "C" ABI of libnfn_hip.so (include/nfn.h): argument
+// validation, the flow program (reversed parameter layout,
+// estimators/DistributionLayers.py:270-277), kernel selection and launch.
+#include <string>
+
+#include "nfn_launch.h"
+
+#define NFN_VERSION_NUM 100  // 0.1.0
+
+namespace nfn {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int32_t param_size(int32_t id, int32_t d) {
+  switch (id) {
+    case NFN_FLOW_PLANAR: return 2 * d + 1;
+    case NFN_FLOW_RADIAL: return d + 2;
+    case NFN_FLOW_AFFINE: return 2 * d;
+    default: return -1;
+  }
+}
+
+int g_math_mode = [] {
+  const char* e = getenv("NFN_MATH");
+  return (e && strcmp(e, "precise") == 0) ? 1 : 0;
+}();
+
+bool use_fast_math() { return g_math_mode == 0; }
+
+// Validates the flow list and fills the program (parameter offsets of the
+// reversed layout, DistributionLayers.py:270-277).  Returns P or < 0.
+int32_t build_program(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable, FlowProgram* prog) {
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims must be in [1, " + std::to_string(NFN_MAX_DIMS) + "]");
+  if (K < 0 || K > NFN_MAX_FLOWS) return fail(NFN_E_FLOW_ID, "number of flows must be in [0, " + std::to_string(NFN_MAX_FLOWS) + "]");
+  if (K > 0 && !flow_ids) return fail(NFN_E_NULLPTR, "flow_ids is NULL");
+  int32_t off = trainable ? 2 * d : 0;
+  // blocks are laid out for flow_types[K-1], ..., flow_types[0]
+  for (int32_t k = K - 1; k >= 0; --k) {
+    const int32_t ps = param_size(flow_ids[k], d);
+    if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_ids[k]));
+    if (prog) prog->step[k] = (off << 2) | flow_ids[k];
+    off += ps;
+  }
+  if (prog) {
+    prog->K = K;
+    for (int q = 0; q < 4; ++q) prog->types[q] = 0;
+    for (int32_t k = 0; k < K; ++k) prog->types[k >> 4] |= (uint32_t)flow_ids[k] << (2 * (k & 15));
+  }
+  return off;
+}
+
+int dm_for(int d) {
+  if (d <= 1) return 1;
+  if (d <= 2) return 2;
+  if (d <= 4) return 4;
+  if (d <= 8) return 8;
+  if (d <= 16) return 16;
+  return 32;
+}
+
+struct TileGeom {
+  int rows;
+  int lds_stride;
+  size_t lds_bytes;
+};
+
+TileGeom tile_geom(int P) {
+  TileGeom g;
+  g.lds_stride = P | 1;  // odd stride: conflict-free per-lane ds_read_b32
+  const size_t row_bytes = (size_t)g.lds_stride * sizeof(float);
+  int rows = kMaxBlock;
+  if (const char* e = getenv("NFN_TILE_ROWS")) {  // tuning knob: 64, 128, 192 or 256
+    const int r = atoi(e);
+    if (r >= 64 && r <= kMaxBlock && r % 64 == 0) rows = r;
+  }
+  while (rows > 64 && (size_t)rows * row_bytes > (size_t)kLdsTileBudget) rows -= 64;
+  g.rows = rows;
+  g.lds_bytes = P > 0 ? (size_t)rows * row_bytes : 0;
+  return g;
+}
+
+// NFN_LOAD_MODE = auto|coop|ownrow|tile|wave selects the tile-streaming strategy
+// (tuning / tests); auto = the measured default.
+enum LoadMode { kAuto = 0, kCoop = 1, kOwnRow = 2, kTile = 3, kWave = 4 };
+
+int load_mode_env() {
+  const char* e = getenv("NFN_LOAD_MODE");
+  if (!e) return kAuto;
+  if (!strcmp(e, "coop")) return kCoop;
+  if (!strcmp(e, "ownrow")) return kOwnRow;
+  if (!strcmp(e, "tile")) return kTile;
+  if (!strcmp(e, "wave")) return kWave;
+  return kAuto;
+}
+
+int group_lds_stride(int P, int G) {
+  int Sx = ((P + G - 1) / G) * G;
+  if (((Sx / G) & 1) == 0) Sx += G;  // S / G odd
+  if (G >= 4) {
+    while (Sx % 4) Sx += 2 * G;  // float4 LDS writes (G >= 4: S = G * odd is a multiple of 4)
+  }
+  return Sx;
+}
+
+// Default (G, DPL) per event-size bound DM, and the alternates a tuning run may
+// request with NFN_GROUP_LANES (fast math, plain chain only).
+void group_shape(int dm, int want_g, int* G, int* DPL) {
+  struct Shape { int dm, g, dpl; };
+  static const Shape defaults[] = {{4, 4, 1}, {8, 4, 2}, {16, 4, 4}, {32, 8, 4}};
+  static const Shape alts[] = {{8, 8, 1}, {8, 2, 4}, {16, 8, 2}, {32, 4, 8}};
+  for (const Shape& x : defaults)
+    if (x.dm == dm) { *G = x.g; *DPL = x.dpl; }
+  for (const Shape& x : alts)
+    if (x.dm == dm && x.g == want_g) { *G = x.g; *DPL = x.dpl; }
+}
+
+// One fp64 partial per workgroup at the smallest tile (64 rows).
+int64_t partials_capacity(int64_t B) { return (B + 63) / 64; }
+
+// Draw ranges per tile for the posterior: enough (tile, range) units for ~8
+// workgroups per CU on a 256-CU MI355X, at most 16 ranges.
+constexpr int64_t kPosteriorTargetUnits = 2048;
+int posterior_split(int64_t B, int rows) {
+  const int64_t ntiles = (B + rows - 1) / rows;
+  if (ntiles <= 0) return 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (kPosteriorTargetUnits + ntiles - 1) / ntiles));
+}
+
+int32_t check_hip(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NFN_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return NFN_OK;
+}
+
+int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride, int64_t t_rowstride,
+                  int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                  const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
+                  void* stream, bool posterior) {
+  g_last_error.clear();
+  ChainArgs a;
+  memset(&a, 0, sizeof(a));
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
+  // the flow math, to measure the memory path of the kernel structure alone.
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
+  a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
+  a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
+  if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
+  if (posterior && S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B == 0) {
+    if (out_sum) {
+      if (hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+    }
+    return NFN_OK;
+  }
+  if (!y) return fail(NFN_E_NULLPTR, "y is NULL");
+  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
+  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
+  if (!out && !workspace) return NFN_OK;
+  const TileGeom g = tile_geom(P);
+  a.y = y;
+  a.t = t;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.out = out;
+  a.partials = workspace ? workspace + 1 : nullptr;  // workspace[0] = number of partials
+  a.y_bstride = y_bstride;
+  a.t_rowstride = t_rowstride;
+  a.t_drawstride = t_drawstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = g.lds_stride;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = posterior ? S : 1;
+  a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((t_drawstride & 3) == 0) &&
+           ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  int64_t nblk = (B + g.rows - 1) / g.rows;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  const int dm = dm_for(d);
+  const int Q = P >> 2;
+  const int mode = load_mode_env();
+  int G = 4, DPL = 1;
+  group_shape(dm, env_int("NFN_GROUP_LANES", 0), &G, &DPL);
+  const int nv_group = (Q + G - 1) / G;  // float4 slots per thread: (256/G rows x Q) / 256
+  const bool group_ok = a.vec4 && t_rowstride != 0 && d >= 4 && Q >= 1 && nv_group <= 16 && mode != kTile &&
+                        mode != kCoop && mode != kOwnRow && mode != kWave && env_int("NFN_GROUP", 1) != 0;
+  bool launched_group = false;
+  if (group_ok) {
+    const int R = kMaxBlock / G;
+    a.lds_stride = group_lds_stride(P, G);
+    a.ntiles = (B + R - 1) / R;
+    // + read-ahead pad: inactive lanes may read G * DPL floats past a row's block
+    const size_t lds = (size_t)R * a.lds_stride * sizeof(float) + (G * DPL + 4) * sizeof(float);
+    launched_group = use_fast_math() ? launch_group_fast(posterior, G, DPL, nv_group, a, lds, s, &nblk)
+                                     : launch_group_precise(posterior, G, DPL, nv_group, a, lds, s, &nblk);
+    if (!launched_group) a.lds_stride = g.lds_stride;
+  }
+  const bool persistent = !launched_group && a.vec4 && t_rowstride != 0 && Q >= 1 && Q <= 16 && mode != kTile;
+  if (launched_group) {
+    // launched above
+  } else if (persistent) {
+    const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;  // Q | 64 too (Q <= 16)
+    // default: wave-tile streaming (measured fastest on C2/C5); coop / ownrow on request
+    const bool wave = (mode == kWave || mode == kAuto) && coop_ok && g.rows % 64 == 0;
+    a.ownrow = wave ? 2 : ((mode == kOwnRow || !coop_ok) ? 1 : 0);
+    const int tile_rows = wave ? 64 : g.rows;
+    const size_t lds_p = g.lds_bytes + 16;  // the packed d = 1 chain may read 3 floats past a row
+    nblk = (B + tile_rows - 1) / tile_rows;
+    a.ntiles = nblk;
+    const bool fast = use_fast_math();
+    if (posterior) {
+      // draw split: more (tile, draw-range) units when the batch alone is too small
+      // to fill the chip; needs the split region of the workspace
+      int nsplit = workspace ? std::min(posterior_split(B, tile_rows), S) : 1;
+      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(std::min(env_int("NFN_POST_SPLIT", 1), S),
+                                                             workspace ? posterior_split(B, g.rows) : 1);
+      a.nsplit = nsplit;
+      a.dps = (S + nsplit - 1) / nsplit;
+      a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges
+      a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B));
+      if (fast) launch_persistent_fast(true, dm, Q, a, g.rows, lds_p, s, &nblk);
+      else launch_persistent_precise(true, dm, Q, a, g.rows, lds_p, s, &nblk);
+      if (a.nsplit > 1) {
+        int32_t rc0 = check_hip("posterior kernel launch");
+        if (rc0 != NFN_OK) return rc0;
+        nblk = (B + kMaxBlock - 1) / kMaxBlock;
+        launch_posterior_merge(fast, (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1, s);
+      }
+    } else {
+      if (fast) launch_persistent_fast(false, dm, Q, a, g.rows, lds_p, s, &nblk);
+      else launch_persistent_precise(false, dm, Q, a, g.rows, lds_p, s, &nblk);
+    }
+  } else {
+    const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
+    launch_tile(use_fast_math(), posterior, dm, a, grid, block, g.lds_bytes, s);
+  }
+  int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
+  if (rc != NFN_OK) return rc;
+  if (out_sum) {
+    launch_reduce_partials((const double*)workspace, out_sum, s);
+    rc = check_hip("reduce_partials_kernel launch");
+  }
+  return rc;
+}
+
+}  // namespace
+}  // namespace nfn
+
+using namespace nfn;
+
+extern "C" {
+
+int32_t nfn_version(void) { return NFN_VERSION_NUM; }
+
+const char* nfn_last_error(void) { return g_last_error.c_str(); }
+
+int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream) {
+  g_last_error.clear();
+  if (n < 0) return fail(NFN_E_SHAPE, "n must be >= 0");
+  if (!out || (n > 0 && !in)) return fail(NFN_E_NULLPTR, "in or out is NULL");
+  launch_reduce_f64(in, n, out, reinterpret_cast<hipStream_t>(stream));
+  return check_hip("reduce_f64_kernel launch");
+}
+
+int32_t nfn_set_math_mode(int32_t mode) {
+  if (mode != 0 && mode != 1) return fail(NFN_E_SHAPE, "math mode must be 0 (fast) or 1 (precise)");
+  const int32_t prev = g_math_mode;
+  g_math_mode = mode;
+  return prev;
+}
+
+int32_t nfn_param_size(int32_t flow_id, int32_t d) {
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
+  const int32_t ps = param_size(flow_id, d);
+  return ps < 0 ? fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id)) : ps;
+}
+
+int32_t nfn_total_param_size(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable_base) {
+  return build_program(flow_ids, K, d, trainable_base ? 1 : 0, nullptr);
+}
+
+int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
+  (void)d;
+  (void)P;
+  if (B <= 0) return 0;
+  return 1 + partials_capacity(B);  // [count | partials]
+}
+
+int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
+  if (B <= 0) return 0;
+  // [count | partials | draw-split region: (max, sum) float2 per (range, sample)]
+  return 1 + partials_capacity(B) + (int64_t)posterior_split(B, tile_geom(P < 0 ? 0 : P).rows) * B;
+}
+
+int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream) {
+  g_last_error.clear();
+  if (!workspace || !out) return fail(NFN_E_NULLPTR, "workspace or out is NULL");
+  launch_reduce_partials(workspace, out, reinterpret_cast<hipStream_t>(stream));
+  return check_hip("reduce_partials_kernel launch");
+}
+
+int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B,
+                              int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                              const float* y_mean, const float* y_std, float* out_logp, double* out_sum,
+                              double* workspace, void* stream) {
+  return run_chain(y, y_bstride, t, 0, t_rowstride, 1, B, d, flow_ids, K, trainable_base, y_mean, y_std, out_logp,
+                   out_sum, workspace, stream, false);
+}
+
+int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
+                              int64_t t_rowstride, int32_t S, int64_t B, int32_t d, const int32_t* flow_ids,
+                              int32_t K, int32_t trainable_base, const float* y_mean, const float* y_std,
+                              float* out_lse, double* out_sum, double* workspace, void* stream) {
+  return run_chain(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, flow_ids, K, trainable_base, y_mean, y_std,
+                   out_lse, out_sum, workspace, stream, true);
+}
+
+int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
+                             int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, void* stream) {
+  g_last_error.clear();
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
+  const int32_t ps = param_size(flow_id, d);
+  if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id));
+  if (B < 0 || z_bstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
+  if (z_bstride != 0 && z_bstride < d) return fail(NFN_E_SHAPE, "z batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < ps) return fail(NFN_E_SHAPE, "t row stride < flow param size");
+  if (B == 0 || (!z_out && !ldj_out)) return NFN_OK;
+  if (!z || !t_k) return fail(NFN_E_NULLPTR, "z or t_k is NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  launch_flow(use_fast_math(), dm_for(d), flow_id, z, z_bstride, t_k, t_rowstride, B, d, z_out, ldj_out, s);
+  return check_hip("flow_fwd_ldj_kernel launch");
+}
+
+}  // extern "C"

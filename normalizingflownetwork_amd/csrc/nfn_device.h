@@ -1,5 +1,5 @@
-// nfn_kernels.hip — gfx950 (MI355X) kernels for the conditional normalizing-flow
-// log_prob hot path, and the extern "C" ABI declared in include/nfn.h.
+// nfn_device.h — device code of the gfx950 (MI355X) conditional normalizing-flow
+// log_prob kernels: math, bijectors, chain evaluators and kernel templates.
 //
 // Reference semantics (paths in the reference checkout):
 //   PlanarFlow  estimators/normalizing_flows/PlanarFlow.py:20-80
@@ -11,31 +11,35 @@
 //   posterior   estimators/BayesianNNEstimator.py:65-76, evaluation/scorers.py:13-27
 //
 // Design (DESIGN.md has the full story):
-//   * One workgroup owns a tile of `rows` consecutive samples (one sample per lane).
-//     The tile's parameter rows t[b0 .. b0+rows) are one contiguous HBM region;
-//     the workgroup streams it with coalesced 16-byte loads and writes it to LDS
-//     with an ODD row stride, so the per-lane parameter reads that follow
-//     (ds_read_b32 at a wave-uniform column offset) are bank-conflict free.
-//   * The flow chain is a runtime program (flow type + parameter offset per step,
-//     wave-uniform, read from the kernel arguments by scalar loads).  z and the
-//     running sum of log-det-Jacobians live in VGPRs for the whole chain; nothing
-//     but log_prob (and one fp64 partial sum per workgroup) is written back.
-//   * The event dimension is a template bound DM (1,2,4,8,16,32) with the runtime
-//     d <= DM guarding the unrolled loops, so z stays in registers.
+//   * Persistent kernels walk tiles of consecutive samples.  A tile's parameter
+//     rows are one contiguous HBM region, streamed with coalesced non-temporal
+//     16-byte loads into registers one tile AHEAD of use, then written to LDS with
+//     a bank-conflict-free row stride; each lane then reads its own sample's
+//     parameters from LDS.
+//   * d = 1 (configs C1/C2/C5): one sample per lane, 64-row tiles owned by single
+//     waves (no workgroup barriers), flow types packed 2 bits per flow so block
+//     offsets are scalar arithmetic, next-flow parameter reads overlapped with
+//     the current flow's math.
+//   * d >= 4 (config C3): G-lane groups per sample with DPP butterfly reductions.
+//   * z and the running log|det J| stay in VGPRs for the whole chain; only
+//     log_prob and one fp64 partial sum per workgroup are written back.
+// Kernel templates are instantiated by the launch translation units
+// (nfn_persistent.hip, nfn_group.hip, nfn_tile.hip, nfn_misc.hip); the C ABI and
+// the dispatch live in nfn_api.hip.
+#pragma once
+
 #include <hip/hip_runtime.h>
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
-#include <string>
 
 #include "nfn.h"
 
-#define NFN_VERSION_NUM 100  // 0.1.0
-
-namespace {
+namespace nfn {
 
 constexpr int kMaxBlock = 256;
 constexpr int kLdsTileBudget = 48 * 1024;  // bytes of LDS per workgroup for the tile
@@ -60,7 +64,7 @@ __device__ __forceinline__ float4 load_row4(const float* p) {
 
 struct FlowProgram {
   int32_t K;
-  uint32_t types;               // K <= 16: flow ids, 2 bits each, application order
+  uint32_t types[4];            // flow ids, 2 bits each, application order (64 flows)
   int32_t step[NFN_MAX_FLOWS];  // (param offset << 2) | flow id, application order
 };
 
@@ -178,6 +182,24 @@ __device__ __forceinline__ float f_tanh(float a) {
   } else {
     return tanhf(a);
   }
+}
+
+// Online logsumexp over draws, branch-free: one exp per draw
+// (scorers.py:25 / BayesianNNEstimator.py:75 take scipy / tf logsumexp over axis 0).
+template <bool FAST>
+__device__ __forceinline__ void lse_push(float& m, float& acc, float lp) {
+  const float dlt = lp - m;
+  const float e = f_exp<FAST>(-fabsf(dlt));
+  const bool up = dlt > 0.0f;  // false for NaN
+  const float acc_new = up ? fmaf(acc, e, 1.0f) : acc + e;
+  acc = (lp == -INFINITY) ? acc : acc_new;
+  m = (lp != lp) ? lp : (up ? lp : m);
+}
+
+template <bool FAST>
+__device__ __forceinline__ float lse_finish(float m, float acc, int S) {
+  const float r = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(acc);
+  return r - f_log<FAST>((float)S);
 }
 
 // ---------------------------------------------------------------------------
@@ -433,7 +455,7 @@ __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, con
   const int K = a.prog.K;
   float l2 = 0.0f;  // sum of log2|det J_k|
   if constexpr (PACKED) {
-    if (K > 0) l2 = chain1_fast_packed(z, row, a.prog.types, K, a.P);
+    if (K > 0) l2 = chain1_fast_packed(z, row, a.prog.types[0], K, a.P);
   } else if (K > 0) {
     int st = a.prog.step[0];
     float pc[3];
@@ -595,21 +617,12 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
 #pragma unroll
       for (int j = 0; j < DM; ++j) z[j] = y0[j];
       const float lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
-      // online logsumexp (scorers.py:25 uses scipy.special.logsumexp over axis 0)
-      if (lp > m) {
-        acc = (m == -INFINITY ? 0.0f : acc * f_exp<FAST>(m - lp)) + 1.0f;
-        m = lp;
-      } else if (lp > -INFINITY) {
-        acc += f_exp<FAST>(lp - m);
-      } else if (lp != lp) {
-        m = lp;  // NaN propagates
-      }
+      lse_push<FAST>(m, acc, lp);
     }
   }
   float res = 0.0f;
   if (tid < nr) {
-    res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(acc);
-    res = res - f_log<FAST>((float)a.S);
+    res = lse_finish<FAST>(m, acc, a.S);
     if (a.out) a.out[b0 + tid] = res;
   }
   if (a.partials) {
@@ -795,17 +808,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
           lp = eval_chain1_fast<PACKED>(z[0], tl + lt * S, a) - corr;
         else
           lp = eval_chain<DM, FAST>(z, tl + lt * S, a) - corr;
-        if constexpr (POST) {
-          // online logsumexp over draws (scorers.py:25: scipy logsumexp over axis 0)
-          if (lp > m) {
-            accl = (m == -INFINITY ? 0.0f : accl * f_exp<FAST>(m - lp)) + 1.0f;
-            m = lp;
-          } else if (lp > -INFINITY) {
-            accl += f_exp<FAST>(lp - m);
-          } else if (lp != lp) {
-            m = lp;
-          }
-        }
+        if constexpr (POST) lse_push<FAST>(m, accl, lp);
       }
       if (wave) wave_lds_sync();  // this tile's LDS reads done before the next writes
     }
@@ -817,10 +820,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
         pend_v = accl;
       } else {
         float res = lp;
-        if constexpr (POST) {
-          res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
-          res = res - f_log<FAST>((float)a.S);
-        }
+        if constexpr (POST) res = lse_finish<FAST>(m, accl, a.S);
         pend_b = b0 + lt;
         pend_v = res;
         acc += (double)res;
@@ -914,31 +914,56 @@ __device__ __forceinline__ float gsum(float v) {
   return v;
 }
 
-template <int G, bool FAST>
-__device__ __forceinline__ float planar_step_g(float& z, const float* p, int d, int j, bool act) {
-  const float u = act ? p[j] : 0.0f;
-  const float w = act ? p[d + j] + 1.0f : 0.0f;
-  const float wtu = gsum<G>(w * u);
-  const float nw2 = gsum<G>(w * w);
-  const float wz = gsum<G>(w * z);
+// A G-lane group owns one sample; lane j owns the DPL dimensions
+// j, j + G, ..., j + (DPL-1) G (interleaved, so each per-dimension LDS read by a
+// group touches G consecutive floats).  G trades redundant per-sample scalar
+// work (softplus / tanh / logs are evaluated by every lane of the group) against
+// per-lane vector work (DPL dims each) and tile size.
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int d, int j) {
+  float u[DPL], w[DPL];
+  float swu = 0.0f, sww = 0.0f, swz = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const bool act = j + G * i < d;
+    u[i] = act ? p[j + G * i] : 0.0f;
+    w[i] = act ? p[d + j + G * i] + 1.0f : 0.0f;
+    swu += w[i] * u[i];
+    sww += w[i] * w[i];
+    swz += w[i] * z[i];
+  }
   const float b = p[2 * d];
+  const float wtu = gsum<G>(swu);
+  const float nw2 = gsum<G>(sww);
+  const float wz = gsum<G>(swz);
   const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
   const float norm_w2 = nw2 + 1e-9f;
   const float coef = m_wtu - wtu;
   const float th = f_tanh<FAST>(wz + b);
   const float dth = 1.0f - th * th;
-  const float uh = u + coef * f_div_acc<FAST>(w, norm_w2);  // 0 on inactive lanes
-  z = z + uh * th;
-  const float sdet = gsum<G>(uh * (dth * w));
-  return f_log<FAST>(fabsf(1.0f + sdet));
+  float sd = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const float uh = u[i] + coef * f_div_acc<FAST>(w[i], norm_w2);  // 0 on inactive dims
+    z[i] = z[i] + uh * th;
+    sd += uh * (dth * w[i]);
+  }
+  return f_log<FAST>(fabsf(1.0f + gsum<G>(sd)));
 }
 
-template <int G, bool FAST>
-__device__ __forceinline__ float radial_step_g(float& z, const float* p, int d, int j, bool act) {
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int d, int j) {
   const float alpha = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
   const float beta = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
-  const float g = act ? p[2 + j] : 0.0f;
-  const float r = gsum<G>(act ? fabsf(z - g) : 0.0f);
+  float g[DPL];
+  float sr = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const bool act = j + G * i < d;
+    g[i] = act ? p[2 + j + G * i] : 0.0f;
+    sr += act ? fabsf(z[i] - g[i]) : 0.0f;
+  }
+  const float r = gsum<G>(sr);
   const float yv = alpha + r;
   float h, der_h;
   if constexpr (FAST) {
@@ -950,53 +975,10 @@ __device__ __forceinline__ float radial_step_g(float& z, const float* p, int d, 
   }
   const float ab = alpha * beta;
   const float abh = ab * h;
-  if (act) z = z + abh * (z - g);
-  const float A = 1.0f + abh;
-  const float Bv = A + (ab * der_h) * r;
-  float Ap = 1.0f;
-  for (int i = 1; i < d; ++i) Ap *= A;
-  return f_log<FAST>(Ap * Bv);
-}
-
-template <int G, bool FAST>
-__device__ __forceinline__ float eval_chain_g_rolled(float z, const float* row, const ChainArgs& a, int j);
-
-// Register-parameter forms of the group steps (parameters read ahead of time).
-template <int G, bool FAST>
-__device__ __forceinline__ float planar_g_regs(float& z, float u, float wraw, float b, bool act) {
-  const float w = act ? wraw + 1.0f : 0.0f;
-  u = act ? u : 0.0f;
-  const float wtu = gsum<G>(w * u);
-  const float nw2 = gsum<G>(w * w);
-  const float wz = gsum<G>(w * z);
-  const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
-  const float norm_w2 = nw2 + 1e-9f;
-  const float coef = m_wtu - wtu;
-  const float th = f_tanh<FAST>(wz + b);
-  const float dth = 1.0f - th * th;
-  const float uh = u + coef * f_div_acc<FAST>(w, norm_w2);  // 0 on inactive lanes
-  z = z + uh * th;
-  const float sdet = gsum<G>(uh * (dth * w));
-  return f_log<FAST>(fabsf(1.0f + sdet));
-}
-
-template <int G, bool FAST>
-__device__ __forceinline__ float radial_g_regs(float& z, float a0, float b0, float g, int d, bool act) {
-  const float alpha = softplus_tf<FAST>(0.3f * a0 - 2.0f);
-  const float beta = softplus_tf<FAST>(0.1f * b0 + kLogExpm1One) - 1.0f;
-  const float r = gsum<G>(act ? fabsf(z - g) : 0.0f);
-  const float yv = alpha + r;
-  float h, der_h;
-  if constexpr (FAST) {
-    h = __builtin_amdgcn_rcpf(yv);
-    der_h = -h * h;
-  } else {
-    h = 1.0f / yv;
-    der_h = (-1.0f / yv) / yv;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    if (j + G * i < d) z[i] = z[i] + abh * (z[i] - g[i]);
   }
-  const float ab = alpha * beta;
-  const float abh = ab * h;
-  if (act) z = z + abh * (z - g);
   const float A = 1.0f + abh;
   const float Bv = A + (ab * der_h) * r;
   float Ap = 1.0f;
@@ -1004,115 +986,58 @@ __device__ __forceinline__ float radial_g_regs(float& z, float a0, float b0, flo
   return f_log<FAST>(Ap * Bv);
 }
 
-// Chains of <= 16 flows: packed flow types, scalar offsets, and the next flow's
-// three per-lane parameters read while the current flow is evaluated.
-//   planar: (u_j, w'_j, b) at (j, d+j, 2d); radial: (a, b, gamma_j) at (0, 1, 2+j);
-//   affine: (shift_j, scale'_j) at (j, d+j).
-template <int G, bool FAST>
-__device__ __forceinline__ float chain_g_packed(float& z, float& dimterm, const float* row, const ChainArgs& a,
-                                                int j) {
+// Flow types of the (up to 64-flow) program, 2 bits each, from the 4 packed words.
+__device__ __forceinline__ int flow_type_at(const uint32_t (&tw)[4], int k) {
+  const uint32_t w = k < 16 ? tw[0] : (k < 32 ? tw[1] : (k < 48 ? tw[2] : tw[3]));
+  return (int)((w >> (2 * (k & 15))) & 3u);
+}
+
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row, const ChainArgs& a, int j) {
   const int d = a.d;
   const int K = a.prog.K;
-  const uint32_t types = a.prog.types;
-  const bool act = j < d;
-  auto size_of = [&](int id) { return id == NFN_FLOW_PLANAR ? 2 * d + 1 : (id == NFN_FLOW_RADIAL ? d + 2 : 2 * d); };
-  auto read = [&](int id, int off, float& x1, float& x2, float& x3) {
+  uint32_t tw[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tw[q] = a.prog.types[q];
+  float ildj = 0.0f, dimterm = 0.0f;
+  // blocks are stored in reverse application order: off_0 = P - size(f_0), ...
+  int off = a.P;
+  for (int k = 0; k < K; ++k) {
+    const int id = flow_type_at(tw, k);
+    off -= id == NFN_FLOW_PLANAR ? 2 * d + 1 : (id == NFN_FLOW_RADIAL ? d + 2 : 2 * d);
     const float* p = row + off;
-    if (id == NFN_FLOW_RADIAL) {
-      x1 = p[0];
-      x2 = p[1];
-      x3 = p[2 + j];
+    if (id == NFN_FLOW_PLANAR) {
+      ildj = ildj + planar_gd<G, DPL, FAST>(z, p, d, j);
+    } else if (id == NFN_FLOW_RADIAL) {
+      ildj = ildj + radial_gd<G, DPL, FAST>(z, p, d, j);
     } else {
-      x1 = p[j];
-      x2 = p[d + j];
-      x3 = p[2 * d];
-    }
-  };
-  float ildj = 0.0f;
-  int id = (int)(types & 3u);
-  int off = a.P - size_of(id);
-  float c1, c2, c3;
-  read(id, off, c1, c2, c3);
-#pragma unroll 1
-  for (int k = 0; k < 16; ++k) {
-    if (k < K) {
-      const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
-      const int offn = max(off - size_of(idn), 0);
-      float n1, n2, n3;
-      read(idn, offn, n1, n2, n3);
-      if (id == NFN_FLOW_PLANAR) {
-        ildj = ildj + planar_g_regs<G, FAST>(z, c1, c2, c3, act);
-      } else if (id == NFN_FLOW_RADIAL) {
-        ildj = ildj + radial_g_regs<G, FAST>(z, c1, c2, c3, d, act);
-      } else if (act) {
-        const float sc = 1.0f + c2;
-        z = z * sc + c1;
-        dimterm += f_log<FAST>(fabsf(sc));
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) {
+        if (j + G * i < d) {
+          const float sc = 1.0f + p[d + j + G * i];
+          z[i] = z[i] * sc + p[j + G * i];
+          dimterm += f_log<FAST>(fabsf(sc));
+        }
       }
-      id = idn;
-      off = offn;
-      c1 = n1;
-      c2 = n2;
-      c3 = n3;
     }
   }
-  return ildj;
-}
-
-template <int G, bool FAST, bool PACKED>
-__device__ __forceinline__ float eval_chain_g(float z, const float* row, const ChainArgs& a, int j) {
-  if constexpr (PACKED) {
-    const int d = a.d;
-    const bool act = j < d;
-    float dimterm = 0.0f;
-    const float ildj = a.prog.K > 0 ? chain_g_packed<G, FAST>(z, dimterm, row, a, j) : 0.0f;
-    if (act) {
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const int jj = j + G * i;
+    if (jj < d) {
       if (a.trainable) {
-        const float sc = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + j]);
-        const float zz = f_div<FAST>(z - row[j], sc);
+        const float sc = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + jj]);
+        const float zz = f_div<FAST>(z[i] - row[jj], sc);
         dimterm += -0.5f * (zz * zz) - f_log<FAST>(sc);
       } else {
-        dimterm += -0.5f * (z * z);
+        dimterm += -0.5f * (z[i] * z[i]);
       }
-    }
-    return (gsum<G>(dimterm) - kHalfLog2Pi * (float)d) + ildj;
-  } else {
-    return eval_chain_g_rolled<G, FAST>(z, row, a, j);
-  }
-}
-
-template <int G, bool FAST>
-__device__ __forceinline__ float eval_chain_g_rolled(float z, const float* row, const ChainArgs& a, int j) {
-  const int d = a.d;
-  const bool act = j < d;
-  float ildj = 0.0f, dimterm = 0.0f;
-  for (int k = 0; k < a.prog.K; ++k) {
-    const int st = a.prog.step[k];
-    const float* p = row + (st >> 2);
-    const int id = st & 3;
-    if (id == NFN_FLOW_PLANAR) {
-      ildj = ildj + planar_step_g<G, FAST>(z, p, d, j, act);
-    } else if (id == NFN_FLOW_RADIAL) {
-      ildj = ildj + radial_step_g<G, FAST>(z, p, d, j, act);
-    } else if (act) {  // affine: per-dimension log|scale_j|
-      const float sc = 1.0f + p[d + j];
-      z = z * sc + p[j];
-      dimterm += f_log<FAST>(fabsf(sc));
-    }
-  }
-  if (act) {
-    if (a.trainable) {
-      const float sc = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + j]);
-      const float zz = f_div<FAST>(z - row[j], sc);
-      dimterm += -0.5f * (zz * zz) - f_log<FAST>(sc);
-    } else {
-      dimterm += -0.5f * (z * z);
     }
   }
   return (gsum<G>(dimterm) - kHalfLog2Pi * (float)d) + ildj;
 }
 
-template <int G, bool FAST, int NV, bool POST, bool PACKED>
+template <int G, int DPL, bool FAST, int NV, bool POST>
 __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
@@ -1123,6 +1048,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   const int j = tid - sl * G;
   const int Q = a.P >> 2;
   const int S = a.lds_stride;
+  const bool lds4 = (S & 3) == 0;
   const int64_t rs = a.t_rowstride;
   const int ndraw = POST ? a.S : 1;
   // tile-invariant slot map: slot k = float4 (tid + k*T) of the tile
@@ -1136,7 +1062,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     loff[k] = r * S + 4 * c;
   }
   float4 buf[NV];
-  float ybuf = 0.0f;
+  float ybuf[DPL];
   bool issued_once = false;
   auto issue = [&](int64_t tile, int s) {
     const int64_t b0 = tile * R;
@@ -1144,18 +1070,15 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
     if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
     issued_once = true;
-    if (a.nt) {
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        if (srow[k] < nr) buf[k] = load_row4<true>(base + goff[k]);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        if (srow[k] < nr) buf[k] = load_row4<false>(base + goff[k]);
-      }
+    for (int k = 0; k < NV; ++k) {
+      if (srow[k] < nr) buf[k] = load_row4<true>(base + goff[k]);
     }
-    if (s == 0 && sl < nr && j < a.d) ybuf = a.y[(b0 + sl) * a.y_bstride + j];
+    if (s == 0 && sl < nr) {
+#pragma unroll
+      for (int i = 0; i < DPL; ++i)
+        ybuf[i] = (j + G * i < a.d) ? a.y[(b0 + sl) * a.y_bstride + j + G * i] : 0.0f;
+    }
   };
   float corr = 0.0f;
   if (a.y_mean) {
@@ -1169,14 +1092,29 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   for (; tile < a.ntiles; tile += gridDim.x) {
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
-    float z0 = ybuf;
-    if (a.y_mean && j < a.d) z0 = f_div<FAST>(z0 - a.y_mean[j], a.y_std[j]);
+    float z0[DPL];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      const int jj = j + G * i;
+      z0[i] = ybuf[i];
+      if (a.y_mean && jj < a.d) z0[i] = f_div<FAST>(z0[i] - a.y_mean[jj], a.y_std[jj]);
+    }
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = 0; s < ndraw; ++s) {
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        if (srow[k] < nr) *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
+        if (srow[k] < nr) {
+          if (lds4) {
+            *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
+          } else {
+            float* dst = lds + loff[k];
+            dst[0] = buf[k].x;
+            dst[1] = buf[k].y;
+            dst[2] = buf[k].z;
+            dst[3] = buf[k].w;
+          }
+        }
       }
       __syncthreads();
       if (pend_b >= 0) {
@@ -1193,25 +1131,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
       else if (tile + gridDim.x < a.ntiles)
         issue(tile + gridDim.x, 0);
       if (sl < nr) {
-        lp = eval_chain_g<G, FAST, PACKED>(z0, lds + sl * S, a, j) - corr;
-        if constexpr (POST) {
-          if (lp > m) {
-            accl = (m == -INFINITY ? 0.0f : accl * f_exp<FAST>(m - lp)) + 1.0f;
-            m = lp;
-          } else if (lp > -INFINITY) {
-            accl += f_exp<FAST>(lp - m);
-          } else if (lp != lp) {
-            m = lp;
-          }
-        }
+        float z[DPL];
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) z[i] = z0[i];
+        lp = eval_chain_gd<G, DPL, FAST>(z, lds + sl * S, a, j) - corr;
+        if constexpr (POST) lse_push<FAST>(m, accl, lp);
       }
     }
     if (sl < nr && j == 0) {
       float res = lp;
-      if constexpr (POST) {
-        res = (m == -INFINITY || m != m) ? m : m + f_log<FAST>(accl);
-        res = res - f_log<FAST>((float)ndraw);
-      }
+      if constexpr (POST) res = lse_finish<FAST>(m, accl, ndraw);
       pend_b = b0 + sl;
       pend_v = res;
       acc += (double)res;
@@ -1250,514 +1179,4 @@ __global__ void __launch_bounds__(kMaxBlock)
   if (ldj_out) ldj_out[b] = ldj;
 }
 
-// Sums the partials of a self-describing workspace: ws[0] = count, ws[1..count].
-__global__ void __launch_bounds__(1024) reduce_partials_kernel(const double* __restrict__ ws,
-                                                              double* __restrict__ out) {
-  __shared__ double red[1024 / 64];
-  const int64_t n = (int64_t)ws[0];
-  const double* in = ws + 1;
-  constexpr int U = 8;
-  double acc[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) acc[u] = 0.0;
-  const int64_t step = (int64_t)blockDim.x * U;
-  int64_t i = threadIdx.x;
-  for (; i + (U - 1) * (int64_t)blockDim.x < n; i += step) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] += in[i + u * (int64_t)blockDim.x];
-  }
-  for (; i < n; i += blockDim.x) acc[0] += in[i];
-  double s = 0.0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) s += acc[u];
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) out[0] = s;
-}
-
-__global__ void __launch_bounds__(1024) reduce_f64_kernel(const double* __restrict__ in, int64_t n,
-                                                          double* __restrict__ out) {
-  __shared__ double red[1024 / 64];
-  constexpr int U = 8;  // independent loads in flight per thread
-  double acc[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) acc[u] = 0.0;
-  const int64_t step = (int64_t)blockDim.x * U;
-  int64_t i = threadIdx.x;
-  for (; i + (U - 1) * (int64_t)blockDim.x < n; i += step) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] += in[i + u * (int64_t)blockDim.x];
-  }
-  for (; i < n; i += blockDim.x) acc[0] += in[i];
-  double s = 0.0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) s += acc[u];
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) out[0] = s;
-}
-
-// ---------------------------------------------------------------------------
-// Host side
-// ---------------------------------------------------------------------------
-
-thread_local std::string g_last_error;
-
-int32_t fail(int32_t code, const std::string& msg) {
-  g_last_error = msg;
-  return code;
-}
-
-int32_t param_size(int32_t id, int32_t d) {
-  switch (id) {
-    case NFN_FLOW_PLANAR: return 2 * d + 1;
-    case NFN_FLOW_RADIAL: return d + 2;
-    case NFN_FLOW_AFFINE: return 2 * d;
-    default: return -1;
-  }
-}
-
-int g_math_mode = [] {
-  const char* e = getenv("NFN_MATH");
-  return (e && strcmp(e, "precise") == 0) ? 1 : 0;
-}();
-
-bool use_fast_math() { return g_math_mode == 0; }
-
-// Validates the flow list and fills the program (parameter offsets of the
-// reversed layout, DistributionLayers.py:270-277).  Returns P or < 0.
-int32_t build_program(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable, FlowProgram* prog) {
-  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims must be in [1, " + std::to_string(NFN_MAX_DIMS) + "]");
-  if (K < 0 || K > NFN_MAX_FLOWS) return fail(NFN_E_FLOW_ID, "number of flows must be in [0, " + std::to_string(NFN_MAX_FLOWS) + "]");
-  if (K > 0 && !flow_ids) return fail(NFN_E_NULLPTR, "flow_ids is NULL");
-  int32_t off = trainable ? 2 * d : 0;
-  // blocks are laid out for flow_types[K-1], ..., flow_types[0]
-  for (int32_t k = K - 1; k >= 0; --k) {
-    const int32_t ps = param_size(flow_ids[k], d);
-    if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_ids[k]));
-    if (prog) prog->step[k] = (off << 2) | flow_ids[k];
-    off += ps;
-  }
-  if (prog) {
-    prog->K = K;
-    prog->types = 0;
-    for (int32_t k = 0; k < K && k < 16; ++k) prog->types |= (uint32_t)flow_ids[k] << (2 * k);
-  }
-  return off;
-}
-
-int dm_for(int d) {
-  if (d <= 1) return 1;
-  if (d <= 2) return 2;
-  if (d <= 4) return 4;
-  if (d <= 8) return 8;
-  if (d <= 16) return 16;
-  return 32;
-}
-
-struct TileGeom {
-  int rows;
-  int lds_stride;
-  size_t lds_bytes;
-};
-
-TileGeom tile_geom(int P) {
-  TileGeom g;
-  g.lds_stride = P | 1;  // odd stride: conflict-free per-lane ds_read_b32
-  const size_t row_bytes = (size_t)g.lds_stride * sizeof(float);
-  int rows = kMaxBlock;
-  if (const char* e = getenv("NFN_TILE_ROWS")) {  // tuning knob: 64, 128, 192 or 256
-    const int r = atoi(e);
-    if (r >= 64 && r <= kMaxBlock && r % 64 == 0) rows = r;
-  }
-  while (rows > 64 && (size_t)rows * row_bytes > (size_t)kLdsTileBudget) rows -= 64;
-  g.rows = rows;
-  g.lds_bytes = P > 0 ? (size_t)rows * row_bytes : 0;
-  return g;
-}
-
-// Tuning knobs (environment, read once): NFN_LOAD_MODE = auto|coop|ownrow|tile,
-// NFN_WG_PER_CU = workgroups per CU for the persistent kernel (0 = occupancy max).
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-enum LoadMode { kAuto = 0, kCoop = 1, kOwnRow = 2, kTile = 3, kWave = 4 };
-
-int load_mode_env() {
-  const char* e = getenv("NFN_LOAD_MODE");
-  if (!e) return kAuto;
-  if (!strcmp(e, "coop")) return kCoop;
-  if (!strcmp(e, "ownrow")) return kOwnRow;
-  if (!strcmp(e, "tile")) return kTile;
-  if (!strcmp(e, "wave")) return kWave;
-  return kAuto;
-}
-
-int cu_count() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
-  return n;
-}
-
-template <int DM, bool FAST, int NV, bool POST>
-void launch_persistent(const ChainArgs& a0, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
-  ChainArgs a = a0;
-  // the packed-program fast path exists for d = 1 chains of <= 16 flows
-  auto kfn = (DM == 1 && FAST && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
-                 ? chain_persistent_kernel<DM, FAST, NV, POST, DM == 1 && FAST>
-                 : chain_persistent_kernel<DM, FAST, NV, POST, false>;
-  int occ = env_int("NFN_WG_PER_CU", 0);
-  if (occ <= 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, T, lds) != hipSuccess || occ <= 0) occ = 1;
-  }
-  const int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)cu_count() * occ);
-  *grid_out = grid;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
-}
-
-template <int DM, bool FAST, bool POST>
-void launch_persistent_nv(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
-  if (Q <= 2)
-    launch_persistent<DM, FAST, 2, POST>(a, T, lds, s, g);
-  else if (Q <= 4)
-    launch_persistent<DM, FAST, 4, POST>(a, T, lds, s, g);
-  else if (Q <= 8)
-    launch_persistent<DM, FAST, 8, POST>(a, T, lds, s, g);
-  else
-    launch_persistent<DM, FAST, 16, POST>(a, T, lds, s, g);
-}
-
-template <bool FAST, bool POST>
-void launch_persistent_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
-  switch (dm) {
-    case 1: launch_persistent_nv<1, FAST, POST>(Q, a, T, lds, s, g); break;
-    case 2: launch_persistent_nv<2, FAST, POST>(Q, a, T, lds, s, g); break;
-    case 4: launch_persistent_nv<4, FAST, POST>(Q, a, T, lds, s, g); break;
-    case 8: launch_persistent_nv<8, FAST, POST>(Q, a, T, lds, s, g); break;
-    case 16: launch_persistent_nv<16, FAST, POST>(Q, a, T, lds, s, g); break;
-    default: launch_persistent_nv<32, FAST, POST>(Q, a, T, lds, s, g); break;
-  }
-}
-
-// Group kernel geometry: R = 256 / G samples per tile; LDS row stride S >= P with
-// S % G == 0 and S / G odd, so the 32 / G samples of a half-wave start on
-// distinct G-bank groups (conflict-free per-dimension ds_read_b32), and S % 4 == 0
-// for the float4 LDS writes.
-int group_lds_stride(int P, int G) {
-  int Sx = ((P + G - 1) / G) * G;
-  if (((Sx / G) & 1) == 0) Sx += G;
-  while (Sx % 4) Sx += 2 * G;
-  return Sx;
-}
-
-template <int G, bool FAST, int NV, bool POST>
-void launch_group(const ChainArgs& a0, size_t lds, hipStream_t s, int64_t* grid_out) {
-  ChainArgs a = a0;
-  auto kfn = (a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? chain_group_kernel<G, FAST, NV, POST, true>
-                                                                : chain_group_kernel<G, FAST, NV, POST, false>;
-  int occ = env_int("NFN_WG_PER_CU", 0);
-  if (occ <= 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, kMaxBlock, lds) != hipSuccess || occ <= 0) occ = 1;
-  }
-  const int64_t grid = std::min<int64_t>(a.ntiles, (int64_t)cu_count() * occ);
-  *grid_out = grid;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
-}
-
-template <int G, bool FAST, bool POST>
-void launch_group_nv(int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
-  if (nv <= 2)
-    launch_group<G, FAST, 2, POST>(a, lds, s, g);
-  else if (nv <= 4)
-    launch_group<G, FAST, 4, POST>(a, lds, s, g);
-  else if (nv <= 6)
-    launch_group<G, FAST, 6, POST>(a, lds, s, g);
-  else if (nv <= 8)
-    launch_group<G, FAST, 8, POST>(a, lds, s, g);
-  else
-    launch_group<G, FAST, 16, POST>(a, lds, s, g);
-}
-
-template <bool FAST, bool POST>
-void launch_group_g(int G, int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
-  switch (G) {
-    case 4: launch_group_nv<4, FAST, POST>(nv, a, lds, s, g); break;
-    case 8: launch_group_nv<8, FAST, POST>(nv, a, lds, s, g); break;
-    case 16: launch_group_nv<16, FAST, POST>(nv, a, lds, s, g); break;
-    default: launch_group_nv<32, FAST, POST>(nv, a, lds, s, g); break;
-  }
-}
-
-template <int DM, bool FAST>
-void launch_chain(const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool posterior) {
-  if (posterior)
-    hipLaunchKernelGGL((posterior_lse_kernel<DM, FAST>), grid, block, lds, s, a);
-  else
-    hipLaunchKernelGGL((chain_logprob_kernel<DM, FAST>), grid, block, lds, s, a);
-}
-
-template <bool FAST>
-void launch_chain_dm(int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool post) {
-  switch (dm) {
-    case 1: launch_chain<1, FAST>(a, grid, block, lds, s, post); break;
-    case 2: launch_chain<2, FAST>(a, grid, block, lds, s, post); break;
-    case 4: launch_chain<4, FAST>(a, grid, block, lds, s, post); break;
-    case 8: launch_chain<8, FAST>(a, grid, block, lds, s, post); break;
-    case 16: launch_chain<16, FAST>(a, grid, block, lds, s, post); break;
-    default: launch_chain<32, FAST>(a, grid, block, lds, s, post); break;
-  }
-}
-
-// One fp64 partial per workgroup at the smallest tile (64 rows).
-int64_t partials_capacity(int64_t B) { return (B + 63) / 64; }
-
-// Draw ranges per tile for the posterior: enough (tile, range) units for ~8
-// workgroups per CU on a 256-CU MI355X, at most 16 ranges.
-constexpr int64_t kPosteriorTargetUnits = 2048;
-int posterior_split(int64_t B, int rows) {
-  const int64_t ntiles = (B + rows - 1) / rows;
-  if (ntiles <= 0) return 1;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (kPosteriorTargetUnits + ntiles - 1) / ntiles));
-}
-
-int32_t check_hip(const char* what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(NFN_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
-  return NFN_OK;
-}
-
-int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride, int64_t t_rowstride,
-                  int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
-                  const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
-                  void* stream, bool posterior) {
-  g_last_error.clear();
-  ChainArgs a;
-  memset(&a, 0, sizeof(a));
-  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
-  if (P < 0) return P;
-  // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
-  // the flow math, to measure the memory path of the kernel structure alone.
-  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
-  a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
-  a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
-  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
-  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
-  if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
-  if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
-  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
-  if (posterior && S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
-  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (B == 0) {
-    if (out_sum) {
-      if (hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
-    }
-    return NFN_OK;
-  }
-  if (!y) return fail(NFN_E_NULLPTR, "y is NULL");
-  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
-  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
-  if (!out && !workspace) return NFN_OK;
-  const TileGeom g = tile_geom(P);
-  a.y = y;
-  a.t = t;
-  a.y_mean = y_mean;
-  a.y_std = y_std;
-  a.out = out;
-  a.partials = workspace ? workspace + 1 : nullptr;  // workspace[0] = number of partials
-  a.y_bstride = y_bstride;
-  a.t_rowstride = t_rowstride;
-  a.t_drawstride = t_drawstride;
-  a.B = B;
-  a.d = d;
-  a.P = P;
-  a.lds_stride = g.lds_stride;
-  a.trainable = trainable_base ? 1 : 0;
-  a.S = posterior ? S : 1;
-  a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((t_drawstride & 3) == 0) &&
-           ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
-  int64_t nblk = (B + g.rows - 1) / g.rows;
-  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
-  const int dm = dm_for(d);
-  const int Q = P >> 2;
-  const int mode = load_mode_env();
-  const int G = dm;  // lanes per sample for the group kernel
-  const int nv_group = (Q + G - 1) / G;
-  const bool group = a.vec4 && t_rowstride != 0 && d >= 4 && Q >= 1 && nv_group <= 16 && mode != kTile &&
-                     mode != kCoop && mode != kOwnRow && env_int("NFN_GROUP", 1) != 0;
-  const bool persistent = !group && a.vec4 && t_rowstride != 0 && Q >= 1 && Q <= 16 && mode != kTile;
-  if (group) {
-    const int R = kMaxBlock / G;
-    a.lds_stride = group_lds_stride(P, G);
-    a.ntiles = (B + R - 1) / R;
-    const size_t lds = (size_t)R * a.lds_stride * sizeof(float) + (G + 4) * sizeof(float);  // + read-ahead pad
-    const bool fast = use_fast_math();
-    if (posterior) {
-      if (fast) launch_group_g<true, true>(G, nv_group, a, lds, s, &nblk);
-      else launch_group_g<false, true>(G, nv_group, a, lds, s, &nblk);
-    } else {
-      if (fast) launch_group_g<true, false>(G, nv_group, a, lds, s, &nblk);
-      else launch_group_g<false, false>(G, nv_group, a, lds, s, &nblk);
-    }
-  } else if (persistent) {
-    const bool coop_ok = (Q & (Q - 1)) == 0 && g.rows % Q == 0;  // Q | 64 too (Q <= 16)
-    // default: wave-tile streaming (measured fastest on C2/C5); coop / ownrow on request
-    const bool wave = (mode == kWave || mode == kAuto) && coop_ok && g.rows % 64 == 0;
-    a.ownrow = wave ? 2 : ((mode == kOwnRow || !coop_ok) ? 1 : 0);
-    const int tile_rows = wave ? 64 : g.rows;
-    const size_t lds_p = g.lds_bytes + 16;  // the packed d = 1 chain may read 3 floats past a row
-    nblk = (B + tile_rows - 1) / tile_rows;
-    a.ntiles = nblk;
-    const bool fast = use_fast_math();
-    if (posterior) {
-      // draw split: more (tile, draw-range) units when the batch alone is too small
-      // to fill the chip; needs the split region of the workspace
-      int nsplit = workspace ? std::min(posterior_split(B, tile_rows), S) : 1;
-      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(std::min(env_int("NFN_POST_SPLIT", 1), S),
-                                                             workspace ? posterior_split(B, g.rows) : 1);
-      a.nsplit = nsplit;
-      a.dps = (S + nsplit - 1) / nsplit;
-      a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges
-      a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B));
-      if (fast) launch_persistent_dm<true, true>(dm, Q, a, g.rows, lds_p, s, &nblk);
-      else launch_persistent_dm<false, true>(dm, Q, a, g.rows, lds_p, s, &nblk);
-      if (a.nsplit > 1) {
-        int32_t rc0 = check_hip("posterior kernel launch");
-        if (rc0 != NFN_OK) return rc0;
-        nblk = (B + kMaxBlock - 1) / kMaxBlock;
-        if (fast)
-          hipLaunchKernelGGL(posterior_merge_kernel<true>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s,
-                             (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1);
-        else
-          hipLaunchKernelGGL(posterior_merge_kernel<false>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s,
-                             (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1);
-      }
-    } else {
-      if (fast) launch_persistent_dm<true, false>(dm, Q, a, g.rows, lds_p, s, &nblk);
-      else launch_persistent_dm<false, false>(dm, Q, a, g.rows, lds_p, s, &nblk);
-    }
-  } else {
-    const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
-    if (use_fast_math())
-      launch_chain_dm<true>(dm, a, grid, block, g.lds_bytes, s, posterior);
-    else
-      launch_chain_dm<false>(dm, a, grid, block, g.lds_bytes, s, posterior);
-  }
-  int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
-  if (rc != NFN_OK) return rc;
-  if (out_sum) {
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(1024), 0, s, (const double*)workspace, out_sum);
-    rc = check_hip("reduce_partials_kernel launch");
-  }
-  return rc;
-}
-
-}  // namespace
-
-extern "C" {
-
-int32_t nfn_version(void) { return NFN_VERSION_NUM; }
-
-const char* nfn_last_error(void) { return g_last_error.c_str(); }
-
-int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream) {
-  g_last_error.clear();
-  if (n < 0) return fail(NFN_E_SHAPE, "n must be >= 0");
-  if (!out || (n > 0 && !in)) return fail(NFN_E_NULLPTR, "in or out is NULL");
-  hipLaunchKernelGGL(reduce_f64_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), in, n, out);
-  return check_hip("reduce_f64_kernel launch");
-}
-
-int32_t nfn_set_math_mode(int32_t mode) {
-  if (mode != 0 && mode != 1) return fail(NFN_E_SHAPE, "math mode must be 0 (fast) or 1 (precise)");
-  const int32_t prev = g_math_mode;
-  g_math_mode = mode;
-  return prev;
-}
-
-int32_t nfn_param_size(int32_t flow_id, int32_t d) {
-  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
-  const int32_t ps = param_size(flow_id, d);
-  return ps < 0 ? fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id)) : ps;
-}
-
-int32_t nfn_total_param_size(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable_base) {
-  return build_program(flow_ids, K, d, trainable_base ? 1 : 0, nullptr);
-}
-
-int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
-  (void)d;
-  (void)P;
-  if (B <= 0) return 0;
-  return 1 + partials_capacity(B);  // [count | partials]
-}
-
-int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
-  if (B <= 0) return 0;
-  // [count | partials | draw-split region: (max, sum) float2 per (range, sample)]
-  return 1 + partials_capacity(B) + (int64_t)posterior_split(B, tile_geom(P < 0 ? 0 : P).rows) * B;
-}
-
-int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream) {
-  g_last_error.clear();
-  if (!workspace || !out) return fail(NFN_E_NULLPTR, "workspace or out is NULL");
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
-                     workspace, out);
-  return check_hip("reduce_partials_kernel launch");
-}
-
-int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B,
-                              int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
-                              const float* y_mean, const float* y_std, float* out_logp, double* out_sum,
-                              double* workspace, void* stream) {
-  return run_chain(y, y_bstride, t, 0, t_rowstride, 1, B, d, flow_ids, K, trainable_base, y_mean, y_std, out_logp,
-                   out_sum, workspace, stream, false);
-}
-
-int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
-                              int64_t t_rowstride, int32_t S, int64_t B, int32_t d, const int32_t* flow_ids,
-                              int32_t K, int32_t trainable_base, const float* y_mean, const float* y_std,
-                              float* out_lse, double* out_sum, double* workspace, void* stream) {
-  return run_chain(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, flow_ids, K, trainable_base, y_mean, y_std,
-                   out_lse, out_sum, workspace, stream, true);
-}
-
-int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
-                             int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, void* stream) {
-  g_last_error.clear();
-  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
-  const int32_t ps = param_size(flow_id, d);
-  if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id));
-  if (B < 0 || z_bstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
-  if (z_bstride != 0 && z_bstride < d) return fail(NFN_E_SHAPE, "z batch stride < n_dims");
-  if (t_rowstride != 0 && t_rowstride < ps) return fail(NFN_E_SHAPE, "t row stride < flow param size");
-  if (B == 0 || (!z_out && !ldj_out)) return NFN_OK;
-  if (!z || !t_k) return fail(NFN_E_NULLPTR, "z or t_k is NULL");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
-  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
-  const dim3 grid((unsigned)nblk), block(kMaxBlock);
-#define NFN_LAUNCH_FLOW(DMV, FASTV)                                                                      \
-  hipLaunchKernelGGL((flow_fwd_ldj_kernel<DMV, FASTV>), grid, block, 0, s, flow_id, z, z_bstride, t_k, \
-                     t_rowstride, B, d, z_out, ldj_out)
-#define NFN_LAUNCH_FLOW_DM(FASTV)             \
-  switch (dm_for(d)) {                        \
-    case 1: NFN_LAUNCH_FLOW(1, FASTV); break;   \
-    case 2: NFN_LAUNCH_FLOW(2, FASTV); break;   \
-    case 4: NFN_LAUNCH_FLOW(4, FASTV); break;   \
-    case 8: NFN_LAUNCH_FLOW(8, FASTV); break;   \
-    case 16: NFN_LAUNCH_FLOW(16, FASTV); break; \
-    default: NFN_LAUNCH_FLOW(32, FASTV); break; \
-  }
-  if (use_fast_math()) {
-    NFN_LAUNCH_FLOW_DM(true)
-  } else {
-    NFN_LAUNCH_FLOW_DM(false)
-  }
-#undef NFN_LAUNCH_FLOW_DM
-#undef NFN_LAUNCH_FLOW
-  return check_hip("flow_fwd_ldj_kernel launch");
-}
-
-}  // extern "C"
+}  // namespace nfn

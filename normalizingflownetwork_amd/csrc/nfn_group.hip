@@ -1,0 +1,66 @@
+// nfn_group.hip — instantiations of chain_group_kernel (d >= 4).
+// Compiled twice: -DNFN_FAST=1 and -DNFN_FAST=0.
+#include "nfn_launch.h"
+
+#ifndef NFN_FAST
+#error "compile with -DNFN_FAST=0 or -DNFN_FAST=1"
+#endif
+
+namespace nfn {
+namespace {
+
+constexpr bool kFast = NFN_FAST != 0;
+
+template <int G, int DPL, int NV, bool POST>
+void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = chain_group_kernel<G, DPL, kFast, NV, POST>;
+  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, a.ntiles);
+  *grid_out = grid;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+}
+
+template <int G, int DPL, bool POST>
+bool launch_g_nv(int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
+  if (nv <= 4)
+    launch_g<G, DPL, 4, POST>(a, lds, s, g);
+  else if (nv <= 8)
+    launch_g<G, DPL, 8, POST>(a, lds, s, g);
+  else if (nv <= 12)
+    launch_g<G, DPL, 12, POST>(a, lds, s, g);
+  else if (nv <= 16)
+    launch_g<G, DPL, 16, POST>(a, lds, s, g);
+  else
+    return false;
+  return true;
+}
+
+template <bool POST>
+bool launch_g_shape(int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
+  // default shapes per event-size bound (see group_shape in nfn_api.hip)
+  if (G == 4 && DPL == 1) return launch_g_nv<4, 1, POST>(nv, a, lds, s, g);
+  if (G == 4 && DPL == 2) return launch_g_nv<4, 2, POST>(nv, a, lds, s, g);
+  if (G == 4 && DPL == 4) return launch_g_nv<4, 4, POST>(nv, a, lds, s, g);
+  if (G == 8 && DPL == 4) return launch_g_nv<8, 4, POST>(nv, a, lds, s, g);
+  // alternates for tuning runs (fast math, plain chain)
+  if constexpr (kFast && !POST) {
+    if (G == 8 && DPL == 1) return launch_g_nv<8, 1, POST>(nv, a, lds, s, g);
+    if (G == 2 && DPL == 4) return launch_g_nv<2, 4, POST>(nv, a, lds, s, g);
+    if (G == 8 && DPL == 2) return launch_g_nv<8, 2, POST>(nv, a, lds, s, g);
+    if (G == 4 && DPL == 8) return launch_g_nv<4, 8, POST>(nv, a, lds, s, g);
+  }
+  return false;
+}
+
+}  // namespace
+
+#if NFN_FAST
+bool launch_group_fast(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
+                       int64_t* grid) {
+#else
+bool launch_group_precise(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
+                          int64_t* grid) {
+#endif
+  return post ? launch_g_shape<true>(G, DPL, nv, a, lds, s, grid) : launch_g_shape<false>(G, DPL, nv, a, lds, s, grid);
+}
+
+}  // namespace nfn

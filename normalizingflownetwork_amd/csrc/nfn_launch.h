@@ -1,0 +1,59 @@
+// nfn_launch.h — host-side launch wrappers shared by the translation units.
+// Each wrapper instantiates its kernel templates in exactly one .hip file so the
+// instantiations compile in parallel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "nfn_device.h"
+
+namespace nfn {
+
+// Tuning / diagnostic knobs (environment, read per launch).
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+inline int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  return n;
+}
+
+// Persistent grid: CUs x resident workgroups (occupancy query, or NFN_WG_PER_CU).
+template <typename K>
+inline int64_t persistent_grid(K kfn, int threads, size_t lds, int64_t units) {
+  int occ = env_int("NFN_WG_PER_CU", 0);
+  if (occ <= 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, threads, lds) != hipSuccess || occ <= 0) occ = 1;
+  }
+  return std::min<int64_t>(units, (int64_t)cu_count() * occ);
+}
+
+// nfn_persistent.hip (compiled once per math mode)
+bool launch_persistent_fast(bool post, int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s,
+                            int64_t* grid);
+bool launch_persistent_precise(bool post, int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s,
+                               int64_t* grid);
+// nfn_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance
+bool launch_group_fast(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
+                       int64_t* grid);
+bool launch_group_precise(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
+                          int64_t* grid);
+// nfn_tile.hip
+void launch_tile(bool fast, bool post, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s);
+void launch_flow(bool fast, int dm, int32_t flow_id, const float* z, int64_t z_bstride, const float* tk,
+                 int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, hipStream_t s);
+// nfn_misc.hip
+void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
+void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);
+void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,
+                            hipStream_t s);
+
+}  // namespace nfn

@@ -1,0 +1,66 @@
+// nfn_persistent.hip — instantiations of chain_persistent_kernel (d <= 32, P <= 64).
+// Compiled twice: -DNFN_FAST=1 (fast transcendentals) and -DNFN_FAST=0 (precise).
+#include "nfn_launch.h"
+
+#ifndef NFN_FAST
+#error "compile with -DNFN_FAST=0 or -DNFN_FAST=1"
+#endif
+
+namespace nfn {
+namespace {
+
+constexpr bool kFast = NFN_FAST != 0;
+
+template <int DM, int NV, bool POST>
+void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
+  // the packed-program fast path exists for d = 1 chains of <= 16 flows
+  auto kfn = (DM == 1 && kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
+                 ? chain_persistent_kernel<DM, kFast, NV, POST, DM == 1 && kFast>
+                 : chain_persistent_kernel<DM, kFast, NV, POST, false>;
+  const int64_t grid = persistent_grid(kfn, T, lds, a.ntiles);
+  *grid_out = grid;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
+}
+
+template <int DM, bool POST>
+void launch_p_nv(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
+  if (Q <= 2)
+    launch_p<DM, 2, POST>(a, T, lds, s, g);
+  else if (Q <= 4)
+    launch_p<DM, 4, POST>(a, T, lds, s, g);
+  else if (Q <= 8)
+    launch_p<DM, 8, POST>(a, T, lds, s, g);
+  else
+    launch_p<DM, 16, POST>(a, T, lds, s, g);
+}
+
+template <bool POST>
+void launch_p_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
+  switch (dm) {
+    case 1: launch_p_nv<1, POST>(Q, a, T, lds, s, g); break;
+    case 2: launch_p_nv<2, POST>(Q, a, T, lds, s, g); break;
+    case 4: launch_p_nv<4, POST>(Q, a, T, lds, s, g); break;
+    case 8: launch_p_nv<8, POST>(Q, a, T, lds, s, g); break;
+    case 16: launch_p_nv<16, POST>(Q, a, T, lds, s, g); break;
+    default: launch_p_nv<32, POST>(Q, a, T, lds, s, g); break;
+  }
+}
+
+}  // namespace
+
+#if NFN_FAST
+bool launch_persistent_fast(bool post, int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s,
+                            int64_t* grid) {
+#else
+bool launch_persistent_precise(bool post, int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s,
+                               int64_t* grid) {
+#endif
+  if (Q < 1 || Q > 16) return false;
+  if (post)
+    launch_p_dm<true>(dm, Q, a, T, lds, s, grid);
+  else
+    launch_p_dm<false>(dm, Q, a, T, lds, s, grid);
+  return true;
+}
+
+}  // namespace nfn

@@ -76,14 +76,17 @@ def run(cfg, variants, reps=20, rounds=3):
 def main():
     which = sys.argv[1:] or ["C2"]
     if which[0] == "c3":  # wide-event group kernel
-        v = [{"name": "auto", "env": {}},
-             {"name": "rolled", "env": {"NFN_PACKED": 0}},
+        v = [{"name": "auto_g4x2", "env": {}},
+             {"name": "g8x1", "env": {"NFN_GROUP_LANES": 8}},
+             {"name": "g2x4", "env": {"NFN_GROUP_LANES": 2}},
              {"name": "tile", "env": {"NFN_LOAD_MODE": "tile"}},
              {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
              {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
-             {"name": "wg4", "env": {"NFN_WG_PER_CU": 4}},
-             {"name": "wg6", "env": {"NFN_WG_PER_CU": 6}},
-             {"name": "wg8", "env": {"NFN_WG_PER_CU": 8}}]
+             {"name": "g8_compute_only", "env": {"NFN_GROUP_LANES": 8, "NFN_ABLATE_LOADS": 1}},
+             {"name": "g2_compute_only", "env": {"NFN_GROUP_LANES": 2, "NFN_ABLATE_LOADS": 1}},
+             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "precise", "env": {}, "math": "precise"}]
         run("C3", v)
         return
     if which[0] == "valu":  # compute vs memory floors
