@@ -117,7 +117,7 @@ int group_lds_stride(int P, int G) {
 void group_shape(int dm, int want_g, int* G, int* DPL) {
   struct Shape { int dm, g, dpl; };
   static const Shape defaults[] = {{4, 4, 1}, {8, 4, 2}, {16, 4, 4}, {32, 8, 4}};
-  static const Shape alts[] = {{8, 8, 1}, {8, 2, 4}, {16, 8, 2}, {32, 4, 8}};
+  static const Shape alts[] = {{8, 8, 1}, {16, 8, 2}};
   for (const Shape& x : defaults)
     if (x.dm == dm) { *G = x.g; *DPL = x.dpl; }
   for (const Shape& x : alts)

@@ -674,8 +674,10 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
   const int r0 = own ? lt : lt / Q;
   const int c4 = own ? 0 : lt - (lt / Q) * Q;
   const int rstep = own ? 0 : TR / Q;
-  const int64_t g0 = (int64_t)r0 * rs + 4 * c4;
-  const int64_t gstep = own ? 4 : (int64_t)rstep * rs;
+  // per-lane offsets inside a tile fit 32 bits (TR * rs floats); the tile base is
+  // wave-uniform, so loads take the SGPR-base + 32-bit VGPR-offset form
+  const uint32_t g0 = (uint32_t)(r0 * rs + 4 * c4);
+  const uint32_t gstep = own ? 4u : (uint32_t)(rstep * rs);
   const int l0 = r0 * S + 4 * c4;
   const int lstep = own ? 4 : rstep * S;
   // Work units: (tile, draw range).  The plain chain has one draw and one range;
@@ -714,12 +716,12 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     if (a.nt) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<true>(base + g0 + k * gstep);
+        if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<true>(base + (g0 + (uint32_t)k * gstep));
       }
     } else {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<false>(base + g0 + k * gstep);
+        if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<false>(base + (g0 + (uint32_t)k * gstep));
       }
     }
     if (first && lt < nr) {
@@ -1051,16 +1053,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   const bool lds4 = (S & 3) == 0;
   const int64_t rs = a.t_rowstride;
   const int ndraw = POST ? a.S : 1;
-  // tile-invariant slot map: slot k = float4 (tid + k*T) of the tile
-  int srow[NV], goff[NV], loff[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int q = tid + k * T;
-    const int r = q / Q, c = q - (q / Q) * Q;
-    srow[k] = (q < R * Q) ? r : 0x7fffffff;
-    goff[k] = (int)(r * rs) + 4 * c;
-    loff[k] = r * S + 4 * c;
-  }
+  // tile-invariant slot map: slot k = float4 q = tid + k*T of the tile, i.e. row
+  // r_k = q / Q, piece c_k = q % Q; stepped incrementally (T = sq*Q + sc) so no
+  // per-slot registers are kept
+  const int r00 = tid / Q, c00 = tid - (tid / Q) * Q;
+  const int sq = T / Q, sc = T - (T / Q) * Q;
+  const int nslots = R * Q;  // float4 pieces per tile
   float4 buf[NV];
   float ybuf[DPL];
   bool issued_once = false;
@@ -1070,9 +1068,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
     if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
     issued_once = true;
+    int r = r00, c = c00;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      if (srow[k] < nr) buf[k] = load_row4<true>(base + goff[k]);
+      if (tid + k * T < nslots && r < nr) buf[k] = load_row4<true>(base + (uint32_t)(r * rs + 4 * c));
+      r += sq;
+      c += sc;
+      if (c >= Q) {
+        c -= Q;
+        r += 1;
+      }
     }
     if (s == 0 && sl < nr) {
 #pragma unroll
@@ -1102,17 +1107,26 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = 0; s < ndraw; ++s) {
       __syncthreads();
+      {
+        int r = r00, c = c00;
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        if (srow[k] < nr) {
-          if (lds4) {
-            *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
-          } else {
-            float* dst = lds + loff[k];
-            dst[0] = buf[k].x;
-            dst[1] = buf[k].y;
-            dst[2] = buf[k].z;
-            dst[3] = buf[k].w;
+        for (int k = 0; k < NV; ++k) {
+          if (tid + k * T < nslots && r < nr) {
+            float* dst = lds + r * S + 4 * c;
+            if (lds4) {
+              *reinterpret_cast<float4*>(dst) = buf[k];
+            } else {
+              dst[0] = buf[k].x;
+              dst[1] = buf[k].y;
+              dst[2] = buf[k].z;
+              dst[3] = buf[k].w;
+            }
+          }
+          r += sq;
+          c += sc;
+          if (c >= Q) {
+            c -= Q;
+            r += 1;
           }
         }
       }

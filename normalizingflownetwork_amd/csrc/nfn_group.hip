@@ -19,12 +19,20 @@ void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) 
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
 }
 
+// float4 slots per thread: the exact count for the common widths (every slot is a
+// live register), rounded up otherwise
 template <int G, int DPL, bool POST>
 bool launch_g_nv(int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
   if (nv <= 4)
     launch_g<G, DPL, 4, POST>(a, lds, s, g);
+  else if (nv <= 5)
+    launch_g<G, DPL, 5, POST>(a, lds, s, g);
+  else if (nv <= 6)
+    launch_g<G, DPL, 6, POST>(a, lds, s, g);
   else if (nv <= 8)
     launch_g<G, DPL, 8, POST>(a, lds, s, g);
+  else if (nv <= 9)
+    launch_g<G, DPL, 9, POST>(a, lds, s, g);
   else if (nv <= 12)
     launch_g<G, DPL, 12, POST>(a, lds, s, g);
   else if (nv <= 16)
@@ -44,9 +52,7 @@ bool launch_g_shape(int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipS
   // alternates for tuning runs (fast math, plain chain)
   if constexpr (kFast && !POST) {
     if (G == 8 && DPL == 1) return launch_g_nv<8, 1, POST>(nv, a, lds, s, g);
-    if (G == 2 && DPL == 4) return launch_g_nv<2, 4, POST>(nv, a, lds, s, g);
     if (G == 8 && DPL == 2) return launch_g_nv<8, 2, POST>(nv, a, lds, s, g);
-    if (G == 4 && DPL == 8) return launch_g_nv<4, 8, POST>(nv, a, lds, s, g);
   }
   return false;
 }
