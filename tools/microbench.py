@@ -89,6 +89,15 @@ def main():
              {"name": "precise", "env": {}, "math": "precise"}]
         run("C3", v)
         return
+    if which[0] == "pf2":  # prefetch depth study (C2)
+        v = [{"name": "depth1", "env": {}},
+             {"name": "depth2", "env": {"NFN_PREFETCH2": 1}},
+             {"name": "depth2_ablate", "env": {"NFN_PREFETCH2": 1, "NFN_ABLATE_FLOWS": 1}},
+             {"name": "depth1_ablate", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "depth2_wg2", "env": {"NFN_PREFETCH2": 1, "NFN_WG_PER_CU": 2}},
+             {"name": "depth2_wg4", "env": {"NFN_PREFETCH2": 1, "NFN_WG_PER_CU": 4}}]
+        run("C2", v)
+        return
     if which[0] == "valu":  # compute vs memory floors
         for cfg in ("C2", "C5"):
             W = {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}
