@@ -115,13 +115,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
     args = ap.parse_args()
 
-    rank, world, local_rank = init_from_env()
+    rank, world, local_rank = init_from_env(backend=args.backend)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     ops.set_math_mode(args.math)
 
     ft, d, B, S = CONFIGS[args.config]
@@ -147,7 +150,12 @@ def main():
         if world > 1:
             red[0:1].copy_(s)
             red[1] = float(B)
-            dist.all_reduce(red)
+            if args.backend == "nccl":
+                dist.all_reduce(red)
+            else:  # gloo reduces host tensors
+                h = red.cpu()
+                dist.all_reduce(h)
+                red.copy_(h)
 
     for _ in range(args.warmup):
         step()
@@ -163,13 +171,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     if world > 1:
-        kt = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+        kt = torch.tensor([kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
     mean_ll = float(red[0].item() / red[1].item()) if world > 1 else float(launcher.sum.item()) / B

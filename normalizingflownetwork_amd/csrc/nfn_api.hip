@@ -127,13 +127,15 @@ void group_shape(int dm, int want_g, int* G, int* DPL) {
 // One fp64 partial per workgroup at the smallest tile (64 rows).
 int64_t partials_capacity(int64_t B) { return (B + 63) / 64; }
 
-// Draw ranges per tile for the posterior: enough (tile, range) units for ~8
-// workgroups per CU on a 256-CU MI355X, at most 16 ranges.
-constexpr int64_t kPosteriorTargetUnits = 2048;
+// Draw ranges per tile for the posterior: enough (tile, range) units for every
+// resident team (~2 per team: 8 workgroups of 256 rows, or 32 waves of 64 rows,
+// per CU on a 256-CU MI355X), at most 16 ranges.  Both targets give the same
+// split for a given B, so the workspace size does not depend on the mode.
 int posterior_split(int64_t B, int rows) {
+  const int64_t target = rows >= 256 ? 2048 : 2048 * (256 / rows);
   const int64_t ntiles = (B + rows - 1) / rows;
   if (ntiles <= 0) return 1;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (kPosteriorTargetUnits + ntiles - 1) / ntiles));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (target + ntiles - 1) / ntiles));
 }
 
 int32_t check_hip(const char* what) {

@@ -17,7 +17,7 @@ void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gri
     // experimental depth-2 prefetch (NFN_PREFETCH2=1): d = 1, packed, wave tiles
     if (env_int("NFN_PREFETCH2", 0) == 1 && a.ownrow == 2 && a.prog.K <= 16 && a.y_mean == nullptr) {
       auto k2 = chain_wave2_kernel<NV>;
-      const int64_t grid = persistent_grid(k2, T, lds, a.ntiles);
+      const int64_t grid = persistent_grid(k2, T, lds, (a.ntiles + T / 64 - 1) / (T / 64));
       *grid_out = grid;
       hipLaunchKernelGGL(k2, dim3((unsigned)grid), dim3(T), lds, s, a);
       return;
@@ -27,7 +27,10 @@ void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gri
   auto kfn = (DM == 1 && kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
                  ? chain_persistent_kernel<DM, kFast, NV, POST, DM == 1 && kFast>
                  : chain_persistent_kernel<DM, kFast, NV, POST, false>;
-  const int64_t grid = persistent_grid(kfn, T, lds, a.ntiles);
+  // units = tiles x draw ranges; in wave mode a workgroup runs T/64 units at a time
+  const int64_t units = a.ntiles * (POST ? a.nsplit : 1);
+  const int teams = a.ownrow == 2 ? T / 64 : 1;
+  const int64_t grid = persistent_grid(kfn, T, lds, (units + teams - 1) / teams);
   *grid_out = grid;
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }

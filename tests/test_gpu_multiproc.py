@@ -1,0 +1,38 @@
+"""Multi-process bench path on one GPU: two ranks (both on cuda:0) run bench.py's
+N > 1 step — fused kernel on each rank's own shard + the (sum, count) all-reduce —
+over gloo (RCCL needs one GPU per rank; the 8-GPU nccl run is the driver's)."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_gloo(gpu):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--backend", "gloo", "--batch", str(1 << 18)]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2 * (1 << 18)
+    assert out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0 and out["scaling"] == "weak"
+    # the all-reduced mean covers both ranks' shards (different seeds => finite mean)
+    assert out["mean_log_prob"] == out["mean_log_prob"]
