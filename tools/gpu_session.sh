@@ -41,12 +41,15 @@ for s in $STEPS; do
     bench_nocpu) run bench_nocpu 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
     c3) run bench_c3 300 python bench.py --config C3 --steps 50 --warmup 10 --no-cpu-baseline ;;
     c5) run bench_c5 300 python bench.py --config C5 --steps 20 --warmup 5 --no-cpu-baseline ;;
-    prof)
-      { cd /tmp; run rocprof_c2 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c2" -o c2 -- \
-        python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    prof)  # the same command as the driver's default bench run
+      { cd /tmp; run rocprof_c2 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c2" -o c2 -- \
+        python3 "$ROOT/bench.py"; cd "$ROOT"; } ;;
+    prof_c5)
+      { cd /tmp; run rocprof_c5 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c5" -o c5 -- \
+        python3 "$ROOT/bench.py" --config C5 --no-cpu-baseline; cd "$ROOT"; } ;;
     prof_c3)
-      { cd /tmp; run rocprof_c3 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c3" -o c3 -- \
-        python3 "$ROOT/bench.py" --config C3 --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+      { cd /tmp; run rocprof_c3 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_c3" -o c3 -- \
+        python3 "$ROOT/bench.py" --config C3 --no-cpu-baseline; cd "$ROOT"; } ;;
     pmc)
       { cd /tmp; run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o f -- \
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
