@@ -201,16 +201,16 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   const int mode = load_mode_env();
   int G = 4, DPL = 1;
   group_shape(dm, env_int("NFN_GROUP_LANES", 0), &G, &DPL);
-  const int nv_group = (Q + G - 1) / G;  // float4 slots per thread: (256/G rows x Q) / 256
+  const int nv_group = (Q + G - 1) / G;  // float4 slots per lane: (64/G rows x Q) / 64
   const bool group_ok = a.vec4 && t_rowstride != 0 && d >= 4 && Q >= 1 && nv_group <= 16 && mode != kTile &&
                         mode != kCoop && mode != kOwnRow && mode != kWave && env_int("NFN_GROUP", 1) != 0;
   bool launched_group = false;
   if (group_ok) {
-    const int R = kMaxBlock / G;
+    const int R = 64 / G;  // samples per wave tile
     a.lds_stride = group_lds_stride(P, G);
     a.ntiles = (B + R - 1) / R;
-    // + read-ahead pad: inactive lanes may read G * DPL floats past a row's block
-    const size_t lds = (size_t)R * a.lds_stride * sizeof(float) + (G * DPL + 4) * sizeof(float);
+    // four wave slots; + pad: inactive lanes may read G * DPL floats past a row's block
+    const size_t lds = (size_t)(kMaxBlock / 64) * R * a.lds_stride * sizeof(float) + (G * DPL + 4) * sizeof(float);
     launched_group = use_fast_math() ? launch_group_fast(posterior, G, DPL, nv_group, a, lds, s, &nblk)
                                      : launch_group_precise(posterior, G, DPL, nv_group, a, lds, s, &nblk);
     if (!launched_group) a.lds_stride = g.lds_stride;

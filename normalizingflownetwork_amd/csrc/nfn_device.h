@@ -1123,26 +1123,33 @@ __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row
   return (gsum<G>(dimterm) - kHalfLog2Pi * (float)d) + ildj;
 }
 
+// Each WAVE owns its own tile stream of R = 64 / G samples (no workgroup
+// barriers, as in the d = 1 wave mode): the next tile's rows are prefetched into
+// registers while the current one is evaluated from the wave's LDS slot.
 template <int G, int DPL, bool FAST, int NV, bool POST>
 __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
   const int T = blockDim.x;
-  const int R = T / G;  // samples per tile
   const int tid = threadIdx.x;
-  const int sl = tid / G;
-  const int j = tid - sl * G;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int R = 64 / G;  // samples per wave tile
+  const int sl = lane / G;
+  const int j = lane - sl * G;
   const int Q = a.P >> 2;
   const int S = a.lds_stride;
   const bool lds4 = (S & 3) == 0;
   const int64_t rs = a.t_rowstride;
   const int ndraw = POST ? a.S : 1;
-  // tile-invariant slot map: slot k = float4 q = tid + k*T of the tile, i.e. row
-  // r_k = q / Q, piece c_k = q % Q; stepped incrementally (T = sq*Q + sc) so no
-  // per-slot registers are kept
-  const int r00 = tid / Q, c00 = tid - (tid / Q) * Q;
-  const int sq = T / Q, sc = T - (T / Q) * Q;
-  const int nslots = R * Q;  // float4 pieces per tile
+  float* tl = lds + wid * R * S;
+  // tile-invariant slot map: slot k = float4 q = lane + 64k of the wave tile, i.e.
+  // row q / Q, piece q % Q, stepped incrementally (64 = sq*Q + sc)
+  const int r00 = lane / Q, c00 = lane - (lane / Q) * Q;
+  const int sq = 64 / Q, sc = 64 - (64 / Q) * Q;
+  const int nslots = R * Q;
+  const int64_t u0 = (int64_t)blockIdx.x * (T >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (T >> 6);
   float4 buf[NV];
   float ybuf[DPL];
   bool issued_once = false;
@@ -1155,7 +1162,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     int r = r00, c = c00;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      if (tid + k * T < nslots && r < nr) buf[k] = load_row4<true>(base + (uint32_t)(r * rs + 4 * c));
+      if (lane + k * 64 < nslots && r < nr) buf[k] = load_row4<true>(base + (int64_t)r * rs + 4 * c);
       r += sq;
       c += sc;
       if (c >= Q) {
@@ -1176,9 +1183,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   double acc = 0.0;
   int64_t pend_b = -1;  // deferred store, see chain_persistent_kernel
   float pend_v = 0.0f;
-  int64_t tile = blockIdx.x;
+  int64_t tile = u0;
   if (tile < a.ntiles) issue(tile, 0);
-  for (; tile < a.ntiles; tile += gridDim.x) {
+  for (; tile < a.ntiles; tile += ustep) {
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
     float z0[DPL];
@@ -1190,13 +1197,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     }
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = 0; s < ndraw; ++s) {
-      __syncthreads();
       {
         int r = r00, c = c00;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-          if (tid + k * T < nslots && r < nr) {
-            float* dst = lds + r * S + 4 * c;
+          if (lane + k * 64 < nslots && r < nr) {
+            float* dst = tl + r * S + 4 * c;
             if (lds4) {
               *reinterpret_cast<float4*>(dst) = buf[k];
             } else {
@@ -1214,7 +1220,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
           }
         }
       }
-      __syncthreads();
+      wave_lds_sync();
       if (pend_b >= 0) {
         if (a.out) {
           if (a.nt_store)
@@ -1226,15 +1232,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
       }
       if (s + 1 < ndraw)
         issue(tile, s + 1);
-      else if (tile + gridDim.x < a.ntiles)
-        issue(tile + gridDim.x, 0);
+      else if (tile + ustep < a.ntiles)
+        issue(tile + ustep, 0);
       if (sl < nr) {
         float z[DPL];
 #pragma unroll
         for (int i = 0; i < DPL; ++i) z[i] = z0[i];
-        lp = eval_chain_gd<G, DPL, FAST>(z, lds + sl * S, a, j) - corr;
+        lp = eval_chain_gd<G, DPL, FAST>(z, tl + sl * S, a, j) - corr;
         if constexpr (POST) lse_push<FAST>(m, accl, lp);
       }
+      wave_lds_sync();  // this tile's LDS reads done before the next writes
     }
     if (sl < nr && j == 0) {
       float res = lp;

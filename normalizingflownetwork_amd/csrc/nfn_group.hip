@@ -14,7 +14,7 @@ constexpr bool kFast = NFN_FAST != 0;
 template <int G, int DPL, int NV, bool POST>
 void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
   auto kfn = chain_group_kernel<G, DPL, kFast, NV, POST>;
-  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, a.ntiles);
+  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);  // 4 wave teams per WG
   *grid_out = grid;
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
 }
