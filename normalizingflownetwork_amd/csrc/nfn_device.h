@@ -143,28 +143,16 @@ __device__ __forceinline__ float f_div_acc(float a, float b) {
   }
 }
 
-// log1p(e) for e >= 0.  FAST: log(u) * e / (u - 1) with u = 1 + e (exact for the
-// rounding of u, so relative accuracy is that of log).
-template <bool FAST>
-__device__ __forceinline__ float f_log1p_pos(float e) {
-  if constexpr (FAST) {
-    const float u = 1.0f + e;
-    const float den = u - 1.0f;
-    const float l = __builtin_amdgcn_logf(u) * kLn2;
-    return den == 0.0f ? e : l * (e * __builtin_amdgcn_rcpf(den));
-  } else {
-    return log1pf(e);
-  }
-}
-
 // tf.nn.softplus (TF SoftplusOp): x if x > 13.94, exp(x) if x < -13.94, else log1p(exp(x)).
 template <bool FAST>
 __device__ __forceinline__ float softplus_tf(float x) {
   if constexpr (FAST) {
-    // max(x,0) + log1p(exp(-|x|)): same function, exp argument <= 0.
-    const float e = f_exp<true>(-fabsf(x));
-    const float sp = fmaxf(x, 0.0f) + f_log1p_pos<true>(e);
-    return x > kSoftplusThr ? x : sp;
+    // max(x,0) + ln(1 + e^{-|x|}): same function, exp argument <= 0; absolute
+    // error ~1 ulp of 1, which is what every consumer (-1 + sp + 1e-5, alpha, beta,
+    // 1e-3 + sp) is sensitive to.  Above TF's 13.94 threshold this equals x to
+    // within 1 ulp, so no select is needed.
+    const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+    return fmaf(__builtin_amdgcn_logf(1.0f + e), kLn2, fmaxf(x, 0.0f));
   } else {
     if (x > kSoftplusThr) return x;
     const float e = expf(x);
@@ -176,9 +164,9 @@ __device__ __forceinline__ float softplus_tf(float x) {
 template <bool FAST>
 __device__ __forceinline__ float f_tanh(float a) {
   if constexpr (FAST) {
-    const float e = f_exp<true>(-2.0f * fabsf(a));
-    const float th = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
-    return copysignf(th, a);
+    // 1 - 2 / (1 + e^{2a}): absolute error ~1e-7, saturates to +-1 cleanly.
+    const float E = __builtin_amdgcn_exp2f(a * (2.0f * kLog2e));
+    return 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));
   } else {
     return tanhf(a);
   }
@@ -359,42 +347,42 @@ __device__ __forceinline__ float eval_chain(float (&z)[DM], const float* row, co
 // every softplus consumer here — -1 + softplus + 1e-5, alpha, beta, the base
 // scale — is sensitive to).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float sp_fast1(float x) {
-  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
-  const float sp = fmaxf(x, 0.0f) + __builtin_amdgcn_logf(1.0f + e) * kLn2;
-  return x > kSoftplusThr ? x : sp;
-}
+__device__ __forceinline__ float sp_fast1(float x) { return softplus_tf<true>(x); }
 
-// returns log2|det|
+// The d = 1 bijectors return their Jacobian determinant (the caller accumulates
+// log2|det|); algebra is rearranged for fewer VALU issues, never for less accuracy.
+// Planar (PlanarFlow.py:23-33, :49-53, :72, :78-80):
+//   coef = (-1 + softplus(wtu) + 1e-5) - wtu,  u_hat = u + coef * w / (w^2 + 1e-9)
+//   tanh(x) = 1 - 2 / (1 + e^{2x})
 __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, float b) {
   const float w = wraw + 1.0f;
   const float wtu = w * u;
-  const float nw2 = w * w + 1e-9f;
-  const float m_wtu = (-1.0f + sp_fast1(wtu)) + 1e-5f;
-  const float coef = m_wtu - wtu;
-  const float uh = u + coef * f_div_acc<true>(w, nw2);
-  const float th = f_tanh<true>(w * z + b);
-  z = z + uh * th;
-  const float dth = 1.0f - th * th;
-  return __builtin_amdgcn_logf(fabsf(1.0f + uh * (dth * w)));
+  const float nw2 = fmaf(w, w, 1e-9f);
+  const float coef = sp_fast1(wtu) - (wtu + (1.0f - 1e-5f));
+  const float uh = fmaf(coef, f_div_acc<true>(w, nw2), u);
+  const float E = __builtin_amdgcn_exp2f(fmaf(w, z, b) * (2.0f * kLog2e));
+  const float th = 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));
+  z = fmaf(uh, th, z);
+  return fmaf(uh, fmaf(-th, th, 1.0f) * w, 1.0f);
 }
 
+// Radial (RadialFlow.py:24-33, :45-70) at d = 1: beta = softplus(.) - 1, so
+// alpha * beta = alpha * sp - alpha, and 1 + abh + ab * (-h^2) * r = 1 + abh * (alpha h)
+// because 1 - h r = alpha h.
 __device__ __forceinline__ float radial1_fast(float& z, float a0, float b0, float g) {
-  const float alpha = sp_fast1(0.3f * a0 - 2.0f);
-  const float beta = sp_fast1(0.1f * b0 + kLogExpm1One) - 1.0f;
-  const float r = fabsf(z - g);
-  const float h = __builtin_amdgcn_rcpf(alpha + r);
-  const float ab = alpha * beta;
+  const float alpha = sp_fast1(fmaf(0.3f, a0, -2.0f));
+  const float ab = fmaf(alpha, sp_fast1(fmaf(0.1f, b0, kLogExpm1One)), -alpha);
+  const float dz = z - g;
+  const float h = __builtin_amdgcn_rcpf(alpha + fabsf(dz));
   const float abh = ab * h;
-  z = z + abh * (z - g);
-  const float A = 1.0f + abh;
-  return __builtin_amdgcn_logf(A + (ab * (-h * h)) * r);  // (1+abh)^0 * (...)
+  z = fmaf(abh, dz, z);
+  return fmaf(abh, alpha * h, 1.0f);
 }
 
 __device__ __forceinline__ float affine1_fast(float& z, float sh, float scraw) {
   const float sc = 1.0f + scraw;
-  z = z * sc + sh;
-  return __builtin_amdgcn_logf(fabsf(sc));
+  z = fmaf(z, sc, sh);
+  return sc;
 }
 
 __device__ __forceinline__ void read3(float (&v)[3], const float* row, int st) {
@@ -412,6 +400,18 @@ __device__ __forceinline__ void read3(float (&v)[3], const float* row, int st) {
 // LDS parameter reads, which for flow k+1 are issued before flow k's math.
 __device__ __forceinline__ int size1(int id) { return id == NFN_FLOW_AFFINE ? 2 : 3; }
 
+__device__ __forceinline__ float flow1_fast(int id, float& z, const float (&p)[3]) {
+  if (id == NFN_FLOW_PLANAR) return planar1_fast(z, p[0], p[1], p[2]);
+  if (id == NFN_FLOW_RADIAL) return radial1_fast(z, p[0], p[1], p[2]);
+  return affine1_fast(z, p[0], p[1]);
+}
+
+__device__ __forceinline__ void read3c(float (&v)[3], const float* row, int off) {
+  v[0] = row[off];
+  v[1] = row[off + 1];
+  v[2] = row[off + 2];
+}
+
 __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, uint32_t types, int K, int P) {
   float l2 = 0.0f;
   int id = (int)(types & 3u);
@@ -420,26 +420,15 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
   // tile is padded) so that no control flow separates a read from its use and
   // the waitcnt pass can count the in-order LDS returns instead of draining.
   float pc[3];
-  pc[0] = row[off];
-  pc[1] = row[off + 1];
-  pc[2] = row[off + 2];
+  read3c(pc, row, off);
 #pragma unroll 1
   for (int k = 0; k < 16; ++k) {
     if (k < K) {
       const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
       const int offn = max(off - size1(idn), 0);
       float pn[3];
-      pn[0] = row[offn];
-      pn[1] = row[offn + 1];
-      pn[2] = row[offn + 2];
-      float l;
-      if (id == NFN_FLOW_PLANAR)
-        l = planar1_fast(z, pc[0], pc[1], pc[2]);
-      else if (id == NFN_FLOW_RADIAL)
-        l = radial1_fast(z, pc[0], pc[1], pc[2]);
-      else
-        l = affine1_fast(z, pc[0], pc[1]);
-      l2 += l;
+      read3c(pn, row, offn);
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
       id = idn;
       off = offn;
       pc[0] = pn[0];
@@ -472,7 +461,7 @@ __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, con
         l = radial1_fast(z, pc[0], pc[1], pc[2]);
       else
         l = affine1_fast(z, pc[0], pc[1]);
-      l2 += l;
+      l2 += __builtin_amdgcn_logf(fabsf(l));
       st = stn;
       pc[0] = pn[0];
       pc[1] = pn[1];
@@ -1022,6 +1011,19 @@ __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int 
   const float wtu = gsum<G>(swu);
   const float nw2 = gsum<G>(sww);
   const float wz = gsum<G>(swz);
+  if constexpr (FAST) {
+    // u_hat_i = u_i + (coef / |w|^2) w_i; dth factored out of the det sum.
+    const float c2 = f_div_acc<true>(softplus_tf<true>(wtu) - (wtu + (1.0f - 1e-5f)), nw2 + 1e-9f);
+    const float th = f_tanh<true>(wz + b);
+    float sd = 0.0f;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      const float uh = fmaf(c2, w[i], u[i]);  // 0 on inactive dims
+      z[i] = fmaf(uh, th, z[i]);
+      sd = fmaf(uh, w[i], sd);
+    }
+    return f_log<true>(fabsf(fmaf(fmaf(-th, th, 1.0f), gsum<G>(sd), 1.0f)));
+  }
   const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
   const float norm_w2 = nw2 + 1e-9f;
   const float coef = m_wtu - wtu;
@@ -1050,6 +1052,19 @@ __device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int 
     sr += act ? fabsf(z[i] - g[i]) : 0.0f;
   }
   const float r = gsum<G>(sr);
+  if constexpr (FAST) {
+    // 1 + abh + ab (-h^2) r = 1 + abh (alpha h) since 1 - h r = alpha h;
+    // (1 + abh)^(d-1) through one extra log instead of a runtime product loop.
+    const float h = __builtin_amdgcn_rcpf(alpha + r);
+    const float abh = (alpha * beta) * h;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      if (j + G * i < d) z[i] = fmaf(abh, z[i] - g[i], z[i]);
+    }
+    const float l2 = fmaf((float)(d - 1), __builtin_amdgcn_logf(1.0f + abh),
+                          __builtin_amdgcn_logf(fmaf(abh, alpha * h, 1.0f)));
+    return l2 * kLn2;
+  }
   const float yv = alpha + r;
   float h, der_h;
   if constexpr (FAST) {
