@@ -117,6 +117,9 @@ def main():
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
+    ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
+                    help="N > 1 mean all-reduce: torch.distributed, or the library's own RCCL "
+                         "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
     args = ap.parse_args()
 
     rank, world, local_rank = init_from_env(backend=args.backend)
@@ -139,6 +142,11 @@ def main():
     sh = int(stream.cuda_stream)
     red = torch.zeros((2,), dtype=torch.float64, device=dev)
     evals_per_step = B * (1 if S is None else S)
+    native = None
+    if world > 1 and args.allreduce == "native":
+        from normalizingflownetwork_amd.parallel import NativeComm
+
+        native = NativeComm()
 
     def step(ev0=None, ev1=None):
         if ev0 is not None:
@@ -147,7 +155,9 @@ def main():
         if ev1 is not None:
             ev1.record(stream)
         s = launcher.finish_sum(sh)
-        if world > 1:
+        if native is not None:
+            native.allreduce_mean(s, B, sh)
+        elif world > 1:
             red[0:1].copy_(s)
             red[1] = float(B)
             if args.backend == "nccl":
@@ -181,7 +191,10 @@ def main():
         kt = torch.tensor([kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
-    mean_ll = float(red[0].item() / red[1].item()) if world > 1 else float(launcher.sum.item()) / B
+    if native is not None:
+        mean_ll = float(native.mean.item())
+    else:
+        mean_ll = float(red[0].item() / red[1].item()) if world > 1 else float(launcher.sum.item()) / B
 
     if rank == 0:
         total_evals = evals_per_step * world * args.steps
@@ -222,6 +235,7 @@ def main():
                 "trainable_base": True,
                 "math": args.math,
                 "parallelism": f"dp{world}",
+                "allreduce": None if world == 1 else args.allreduce,
             },
             "roofline": {
                 "bound": "hbm",
@@ -239,6 +253,8 @@ def main():
             "mean_log_prob": mean_ll,
         }
         print(json.dumps(line), flush=True)
+    if native is not None:
+        native.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -40,6 +40,11 @@
  *   nfn_posterior_lse_f32  <- BayesianNNEstimator.score per-sample logsumexp
  *                                                    estimators/BayesianNNEstimator.py:65-76,
  *                                                    evaluation/scorers.py:13-27
+ *   nfn_comm_* /
+ *   nfn_allreduce_mean     <- the mean of score()/mle_log_likelihood_score over a batch
+ *                             sharded across GPUs (one RCCL all-reduce of {sum, count})
+ *                                                    estimators/BaseEstimator.py:43-47,
+ *                                                    evaluation/scorers.py:30-34
  *   nfn_param_size /
  *   nfn_total_param_size   <- Flow.get_param_size    PlanarFlow.py:35-41, RadialFlow.py:36-42,
  *                                                    AffineFlow.py:11-17
@@ -67,6 +72,9 @@ extern "C" {
 #define NFN_E_FLOW_ID -2   /* unknown flow id or too many flows            */
 #define NFN_E_NULLPTR -3   /* required pointer is NULL                     */
 #define NFN_E_HIP -4       /* HIP runtime error (launch, no device, ...)   */
+#define NFN_E_COMM -5      /* RCCL error                                   */
+
+#define NFN_COMM_ID_BYTES 128
 
 /* Library version as MAJOR*10000 + MINOR*100 + PATCH. */
 int32_t nfn_version(void);
@@ -147,6 +155,22 @@ int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t,
                               const int32_t* flow_ids, int32_t K, int32_t trainable_base,
                               const float* y_mean, const float* y_std, float* out_lse, double* out_sum,
                               double* workspace, void* stream);
+
+/*
+ * Multi-GPU (one process per GPU, batch sharded over ranks).  The communicator
+ * is RCCL over xGMI; its handle is opaque (`void*` = ncclComm_t).
+ *   nfn_comm_unique_id : rank 0 creates the 128-byte rendezvous id, which the
+ *                        caller distributes to every rank (any channel).
+ *   nfn_comm_init      : collective over all ranks; binds the CURRENT HIP device.
+ *   nfn_allreduce_mean : sum_count (device double[2]) := sum over ranks of
+ *                        {local_sum[0], local_count}; mean_out (device double[1],
+ *                        nullable) := sum / count.  Stream-ordered, no host sync.
+ */
+int32_t nfn_comm_unique_id(uint8_t* id_out);
+int32_t nfn_comm_init(void** comm_out, int32_t nranks, const uint8_t* id, int32_t rank);
+int32_t nfn_comm_destroy(void* comm);
+int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, double* sum_count,
+                           double* mean_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -43,6 +43,10 @@ SIGNATURES = {
             _vp, _vp, _vp, _vp, _vp, _vp,
         ],
     ),
+    "nfn_comm_unique_id": (_c_int32, [_vp]),
+    "nfn_comm_init": (_c_int32, [ctypes.POINTER(_vp), _c_int32, _vp, _c_int32]),
+    "nfn_comm_destroy": (_c_int32, [_vp]),
+    "nfn_allreduce_mean": (_c_int32, [_vp, _vp, _c_int64, _vp, _vp, _vp]),
 }
 
 # Status codes (include/nfn.h)
@@ -51,6 +55,8 @@ NFN_E_SHAPE = -1
 NFN_E_FLOW_ID = -2
 NFN_E_NULLPTR = -3
 NFN_E_HIP = -4
+NFN_E_COMM = -5
+NFN_COMM_ID_BYTES = 128
 
 _lib = None
 

@@ -29,7 +29,10 @@ UNITS = [
     ("group_precise", "nfn_group.hip", ["-DNFN_FAST=0"]),
     ("tile", "nfn_tile.hip", []),
     ("misc", "nfn_misc.hip", []),
+    ("comm", "nfn_comm.hip", []),
 ]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+LINK_LIBS = ["-L" + os.path.join(ROCM, "lib"), "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-lrccl"]
 SOURCES = sorted({os.path.join(CSRC, u[1]) for u in UNITS})
 
 
@@ -76,7 +79,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda u: _compile(u, verbose), UNITS))
     if force or _stale(OUT, objs):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs + LINK_LIBS
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

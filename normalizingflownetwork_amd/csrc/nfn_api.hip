@@ -8,18 +8,21 @@
 #define NFN_VERSION_NUM 100  // 0.1.0
 
 namespace nfn {
+
+thread_local std::string g_last_error;
+
+int32_t set_error(int32_t code, const char* msg) {
+  g_last_error = msg;
+  return code;
+}
+
 namespace {
 
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
 
-thread_local std::string g_last_error;
-
-int32_t fail(int32_t code, const std::string& msg) {
-  g_last_error = msg;
-  return code;
-}
+int32_t fail(int32_t code, const std::string& msg) { return set_error(code, msg.c_str()); }
 
 int32_t param_size(int32_t id, int32_t d) {
   switch (id) {

@@ -13,6 +13,9 @@
 
 namespace nfn {
 
+// Record `msg` as this thread's nfn_last_error() and return `code` (nfn_api.hip).
+int32_t set_error(int32_t code, const char* msg);
+
 // Tuning / diagnostic knobs (environment, read per launch).
 inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);

@@ -6,10 +6,16 @@ fused kernel, and the ONLY collective is one all-reduce of ``(sum log_prob,
 count)`` in fp64 (16 bytes) — the distributed form of ``score``'s ``.mean()``
 (``BaseEstimator.py:47``, ``scorers.py:34``).  On MI355X the process group is
 ``nccl`` (= RCCL over xGMI); ``gloo`` works for CPU-side tests.
+
+Two interchangeable forms of that all-reduce: ``allreduce_sum_count`` through
+``torch.distributed``, and ``NativeComm`` — the library's own RCCL communicator
+behind the C ABI (``nfn_comm_init`` / ``nfn_allreduce_mean``, include/nfn.h),
+stream-ordered on the device with no host round trip.
 """
 
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -52,6 +58,55 @@ def mean_log_prob(
                                                                                   trainable_base) else 0)
     buf = allreduce_sum_count(s, count, group)
     return buf[0] / buf[1]
+
+
+class NativeComm:
+    """RCCL communicator owned by ``libnfn_hip.so`` (one per process / GPU).
+
+    The 128-byte rendezvous id is made on rank 0 and distributed over the
+    existing ``torch.distributed`` group (any backend); without an initialised
+    group the communicator has one rank.  Binds the current HIP device."""
+
+    def __init__(self, group=None):
+        from . import _lib
+
+        self._lib = _lib.load()
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = (ctypes.c_uint8 * _lib.NFN_COMM_ID_BYTES)()
+        if self.rank == 0:
+            _lib.check(self._lib.nfn_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)), "nfn_comm_unique_id")
+        if self.world > 1:
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0, group=group)
+            uid = (ctypes.c_uint8 * _lib.NFN_COMM_ID_BYTES).from_buffer_copy(box[0])
+        handle = ctypes.c_void_p()
+        _lib.check(self._lib.nfn_comm_init(ctypes.byref(handle), self.world, ctypes.cast(uid, ctypes.c_void_p),
+                                           self.rank), "nfn_comm_init")
+        self.handle = handle
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.sum_count = torch.zeros((2,), dtype=torch.float64, device=dev)
+        self.mean = torch.zeros((1,), dtype=torch.float64, device=dev)
+
+    def allreduce_mean(self, local_sum: torch.Tensor, local_count: int, stream=None) -> torch.Tensor:
+        """``{sum, count}`` summed over ranks into ``self.sum_count``; returns the
+        device scalar ``sum / count`` (``self.mean``).  Stream-ordered."""
+        from . import _lib
+
+        assert local_sum.dtype == torch.float64 and local_sum.is_cuda
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        _lib.check(self._lib.nfn_allreduce_mean(self.handle, local_sum.data_ptr(), int(local_count),
+                                                self.sum_count.data_ptr(), self.mean.data_ptr(), int(stream)),
+                   "nfn_allreduce_mean")
+        return self.mean
+
+    def close(self) -> None:
+        from . import _lib
+
+        if self.handle:
+            _lib.check(self._lib.nfn_comm_destroy(self.handle), "nfn_comm_destroy")
+            self.handle = ctypes.c_void_p()
 
 
 def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:

@@ -110,3 +110,20 @@ def test_python_binding_fails_loudly_without_device(native_lib):
 
     with pytest.raises(RuntimeError):
         ops.chain_log_prob([[0.0]], [[0.0] * 8], ("radial", "radial"), 1, True)
+
+
+def test_comm_entry_points_validate_before_rccl(native_lib):
+    """nfn_comm_init / nfn_allreduce_mean reject bad arguments without touching
+    RCCL or the device (multi-GPU boundary, include/nfn.h)."""
+    from normalizingflownetwork_amd import _lib
+
+    h = ctypes.c_void_p()
+    uid = (ctypes.c_uint8 * _lib.NFN_COMM_ID_BYTES)()
+    p_uid = ctypes.cast(uid, ctypes.c_void_p)
+    assert native_lib.nfn_comm_init(ctypes.byref(h), 0, p_uid, 0) == _lib.NFN_E_SHAPE
+    assert native_lib.nfn_comm_init(ctypes.byref(h), 2, p_uid, 2) == _lib.NFN_E_SHAPE
+    assert native_lib.nfn_comm_init(ctypes.byref(h), 2, None, 0) == _lib.NFN_E_NULLPTR
+    assert native_lib.nfn_comm_unique_id(None) == _lib.NFN_E_NULLPTR
+    assert native_lib.nfn_allreduce_mean(None, None, 1, None, None, None) == _lib.NFN_E_NULLPTR
+    assert "allreduce" in _lib.last_error()
+    assert native_lib.nfn_comm_destroy(None) == _lib.NFN_OK
