@@ -55,6 +55,46 @@ def algorithmic_bytes_per_launch(d: int, P: int, B: int, S) -> float:
     return float(B) * (S * 4 * P + 4 * d + 4)
 
 
+def algorithmic_bytes_grad(d: int, P: int, B: int) -> float:
+    """Fused backward: y (4d) + t (4P) + upstream gradient (4) in, d/dt (4P) + d/dy (4d) out."""
+    return float(B) * (8 * d + 8 * P + 4)
+
+
+def cpu_baseline_grad(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 16) -> dict:
+    """Reference-path stand-in for the backward: the oracle's torch fp32 autodiff through
+    the same eager op sequence (what Keras does when the reference trains), 1 thread."""
+    from oracle import nfn_grad_oracle as G
+
+    ft, d, _, _ = CONFIGS[cfg]
+    P = G.total_param_size(ft, d, True)
+    rng = np.random.default_rng(22)
+    y = rng.standard_normal((sample_rows, d)).astype(np.float32)
+    t = rng.standard_normal((sample_rows, P)).astype(np.float32)
+    g = np.full((sample_rows,), -1.0 / sample_rows, np.float32)
+    nth = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        run = lambda: G.chain_log_prob_grad(y, t, ft, d, True, g_out=g, dtype=np.float32)  # noqa: E731
+        run()
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+    finally:
+        torch.set_num_threads(nth)
+    return {
+        "value": reps * sample_rows / el,
+        "unit": "evals/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{sample_rows} samples of {cfg}, torch fp32 autodiff of the eager op sequence "
+                  f"(oracle/nfn_grad_oracle.py), {reps} reps in {el:.1f}s, 1 thread",
+    }
+
+
 def cpu_baseline(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 20) -> dict:
     """The reference-path stand-in timed on this host: the oracle's fp32 op-by-op
     numpy restatement (whole-batch ops, TF-eager op order) on a bounded slice."""
@@ -117,6 +157,9 @@ def main():
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
+    ap.add_argument("--mode", default="forward", choices=["forward", "grad"],
+                    help="forward = fused log_prob (the headline); grad = the fused backward of the "
+                         "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient)")
     ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
                     help="N > 1 mean all-reduce: torch.distributed, or the library's own RCCL "
                          "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
@@ -137,7 +180,13 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(22 + rank)
     y = torch.randn((B, d), generator=gen, device=dev)
     t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
-    launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
+    grad_mode = args.mode == "grad"
+    if grad_mode:
+        assert S is None, "--mode grad covers the plain chain configs (C2, C3)"
+        g_up = torch.full((B,), -1.0 / B, dtype=torch.float32, device=dev)  # d(mean NLL)/d log_prob
+        launcher = ops.GradLauncher(y, t, ft, d, True, g_out=g_up)
+    else:
+        launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
     red = torch.zeros((2,), dtype=torch.float64, device=dev)
@@ -154,6 +203,8 @@ def main():
         launcher.launch(sh)
         if ev1 is not None:
             ev1.record(stream)
+        if grad_mode:  # per-sample gradients stay on their rank (the MLP's would be all-reduced)
+            return
         s = launcher.finish_sum(sh)
         if native is not None:
             native.allreduce_mean(s, B, sh)
@@ -191,7 +242,9 @@ def main():
         kt = torch.tensor([kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
-    if native is not None:
+    if grad_mode:
+        mean_ll = None
+    elif native is not None:
         mean_ll = float(native.mean.item())
     else:
         mean_ll = float(red[0].item() / red[1].item()) if world > 1 else float(launcher.sum.item()) / B
@@ -199,20 +252,27 @@ def main():
     if rank == 0:
         total_evals = evals_per_step * world * args.steps
         value = total_evals / elapsed
-        bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
+        bytes_launch = algorithmic_bytes_grad(d, P, B) if grad_mode else algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.config, B)
+        traffic, traffic_src = load_traffic(args.config + ("_grad" if grad_mode else ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.config, seconds=args.cpu_seconds)
+            cpu = (cpu_baseline_grad if grad_mode else cpu_baseline)(args.config, seconds=args.cpu_seconds)
         wl = {
             "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
             "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
             "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
         }[args.config]
+        if grad_mode:
+            kernel_name = "chain_grad_kernel"
+            metric = f"log_prob backward evals/sec (whole node), {args.config}"
+        else:
+            kernel_name = {"C2": "chain_persistent_kernel", "C3": "chain_group_kernel",
+                           "C5": "chain_persistent_kernel + posterior_merge_kernel"}[args.config]
+            metric = ("log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"
+                      if args.config == "C2" else f"log_prob evals/sec (whole node), {args.config}")
         line = {
-            "metric": "log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"
-            if args.config == "C2" else f"log_prob evals/sec (whole node), {args.config}",
+            "metric": metric,
             "value": value,
             "unit": "evals/s",
             "n_gpus": world,
@@ -235,7 +295,8 @@ def main():
                 "trainable_base": True,
                 "math": args.math,
                 "parallelism": f"dp{world}",
-                "allreduce": None if world == 1 else args.allreduce,
+                "allreduce": None if (world == 1 or grad_mode) else args.allreduce,
+                "mode": args.mode,
             },
             "roofline": {
                 "bound": "hbm",
@@ -244,7 +305,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "chain_logprob_kernel" if S is None else "posterior_lse_kernel",
+                "kernel": kernel_name,
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "traffic_source": traffic_src,

@@ -32,6 +32,11 @@
  *                             and out_sum feeds score()/mle_log_likelihood_score
  *                                                    estimators/BaseEstimator.py:43-47,
  *                                                    evaluation/scorers.py:30-34
+ *   nfn_chain_logprob_grad_f32
+ *                          <- the gradient Keras autodiff takes through that log_prob when the
+ *                             reference trains: model.compile(loss=NLL) / fit
+ *                                                    estimators/BaseEstimator.py:19-31, 55-59,
+ *                                                    estimators/MaximumLikelihoodNNEstimator.py:33-35
  *   nfn_flow_fwd_ldj_f32   <- PlanarFlow._forward/_forward_log_det_jacobian
  *                                                    estimators/normalizing_flows/PlanarFlow.py:20-80
  *                             RadialFlow._forward/_forward_log_det_jacobian
@@ -118,6 +123,21 @@ int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t,
                               int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
                               int32_t trainable_base, const float* y_mean, const float* y_std,
                               float* out_logp, double* out_sum, double* workspace, void* stream);
+
+/*
+ * Fused backward (the training path).  With L = sum_b g_out[b] * logp[b]
+ * (g_out NULL => all ones), per sample b:
+ *   grad_t[b, :] = dL/dt[b, :]  — (B, P) rows at grad_t_rowstride (>= P), nullable
+ *   grad_y[b, :] = dL/dy[b, :]  — (B, d) contiguous, nullable
+ *   out_logp[b]  = logp[b]      — nullable
+ * Inputs as for nfn_chain_logprob_f32.  A broadcast input (stride 0) still gets one
+ * gradient row per sample; reducing over the batch is the caller's.  y_mean /
+ * y_std are constants here (BaseEstimator.set_data_normalization, not trained).
+ */
+int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
+                                   int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                                   const float* y_mean, const float* y_std, const float* g_out, float* out_logp,
+                                   float* grad_t, int64_t grad_t_rowstride, float* grad_y, void* stream);
 
 /*
  * One bijector, forward direction: z_out = f(z), ldj_out = log|det df/dz| (B,).

@@ -29,6 +29,7 @@ UNITS = [
     ("group_precise", "nfn_group.hip", ["-DNFN_FAST=0"]),
     ("tile", "nfn_tile.hip", []),
     ("misc", "nfn_misc.hip", []),
+    ("grad", "nfn_grad.hip", []),
     ("comm", "nfn_comm.hip", []),
 ]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")

@@ -266,6 +266,59 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   return rc;
 }
 
+int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B, int32_t d,
+                 const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                 const float* y_std, const float* g_out, float* out_logp, float* grad_t, int64_t gt_rowstride,
+                 float* grad_y, void* stream) {
+  g_last_error.clear();
+  GradArgs ga;
+  memset(&ga, 0, sizeof(ga));
+  ChainArgs& a = ga.c;
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (y_bstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
+  if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
+  if (grad_t && gt_rowstride < P) return fail(NFN_E_SHAPE, "grad_t row stride < total param size");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  if (B == 0 || (!out_logp && !grad_t && !grad_y)) return NFN_OK;
+  if (!y) return fail(NFN_E_NULLPTR, "y is NULL");
+  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
+  // Tile geometry: R samples per one-wave workgroup, each with a parameter row
+  // (odd stride) and its K*d flow inputs in LDS.
+  const int S = P | 1;
+  const size_t row_bytes = (size_t)(S + K * d) * sizeof(float);
+  int R = 64;
+  while (R > 1 && (size_t)R * row_bytes > (size_t)64 * 1024) R >>= 1;
+  if ((size_t)R * row_bytes > (size_t)160 * 1024) return fail(NFN_E_SHAPE, "parameter row + flow inputs exceed LDS");
+  const int64_t nblk = (B + R - 1) / R;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  a.y = y;
+  a.t = t;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.out = out_logp;
+  a.y_bstride = y_bstride;
+  a.t_rowstride = t_rowstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = S;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = 1;
+  a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  ga.g_out = g_out;
+  ga.grad_t = grad_t;
+  ga.grad_y = grad_y;
+  ga.gt_rowstride = grad_t ? gt_rowstride : 0;
+  ga.gt_vec4 = ((P & 3) == 0) && ((gt_rowstride & 3) == 0) && ((reinterpret_cast<uintptr_t>(grad_t) & 15) == 0);
+  ga.rows = R;
+  launch_grad(use_fast_math(), dm_for(d), ga, dim3((unsigned)nblk), (size_t)R * row_bytes,
+              reinterpret_cast<hipStream_t>(stream));
+  return check_hip("chain_grad_kernel launch");
+}
+
 }  // namespace
 }  // namespace nfn
 
@@ -336,6 +389,14 @@ int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t,
                               float* out_lse, double* out_sum, double* workspace, void* stream) {
   return run_chain(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, flow_ids, K, trainable_base, y_mean, y_std,
                    out_lse, out_sum, workspace, stream, true);
+}
+
+int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
+                                   int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                                   const float* y_mean, const float* y_std, const float* g_out, float* out_logp,
+                                   float* grad_t, int64_t grad_t_rowstride, float* grad_y, void* stream) {
+  return run_grad(y, y_bstride, t, t_rowstride, B, d, flow_ids, K, trainable_base, y_mean, y_std, g_out, out_logp,
+                  grad_t, grad_t_rowstride, grad_y, stream);
 }
 
 int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,

@@ -96,6 +96,17 @@ struct ChainArgs {
   FlowProgram prog;
 };
 
+// Backward (nfn_grad.hip): the forward's arguments plus the gradient outputs.
+struct GradArgs {
+  ChainArgs c;
+  const float* g_out;    // upstream gradient (B,) or NULL = ones
+  float* grad_t;         // (B, P) at gt_rowstride, or NULL
+  float* grad_y;         // (B, d) contiguous, or NULL
+  int64_t gt_rowstride;
+  int32_t gt_vec4;       // grad_t rows can be written as float4
+  int32_t rows;          // samples per workgroup (<= 64, one wave)
+};
+
 // ---------------------------------------------------------------------------
 // Math.  FAST uses the gfx950 transcendental unit directly (v_exp_f32, v_log_f32,
 // v_rcp_f32) with algebraic rewrites chosen to keep ABSOLUTE error ~1e-7 on every
@@ -439,6 +450,16 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
   return l2;
 }
 
+// Base log-density at d = 1 (fast math), shared by every d = 1 evaluator.
+__device__ __forceinline__ float base1_fast(float z, const float* row, bool trainable) {
+  if (trainable) {
+    const float sc = 1e-3f + sp_fast1(kLogExpm1One + 0.1f * row[1]);
+    const float zz = f_div<true>(z - row[0], sc);
+    return -0.5f * (zz * zz) - (kHalfLog2Pi + __builtin_amdgcn_logf(sc) * kLn2);
+  }
+  return -0.5f * (z * z) - kHalfLog2Pi;
+}
+
 template <bool PACKED>
 __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, const ChainArgs& a) {
   const int K = a.prog.K;
@@ -468,15 +489,7 @@ __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, con
       pc[2] = pn[2];
     }
   }
-  float base;
-  if (a.trainable) {
-    const float sc = 1e-3f + sp_fast1(kLogExpm1One + 0.1f * row[1]);
-    const float zz = f_div<true>(z - row[0], sc);
-    base = -0.5f * (zz * zz) - (kHalfLog2Pi + __builtin_amdgcn_logf(sc) * kLn2);
-  } else {
-    base = -0.5f * (z * z) - kHalfLog2Pi;
-  }
-  return base + l2 * kLn2;
+  return base1_fast(z, row, a.trainable != 0) + l2 * kLn2;
 }
 
 // One evaluator per (DM, FAST) for every kernel, so all tile-streaming strategies

@@ -53,6 +53,8 @@ bool launch_group_precise(bool post, int G, int DPL, int nv, const ChainArgs& a,
 void launch_tile(bool fast, bool post, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 void launch_flow(bool fast, int dm, int32_t flow_id, const float* z, int64_t z_bstride, const float* tk,
                  int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, hipStream_t s);
+// nfn_grad.hip
+void launch_grad(bool fast, int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_t s);
 // nfn_misc.hip
 void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);

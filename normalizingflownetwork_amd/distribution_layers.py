@@ -51,6 +51,10 @@ def _cols(t, begin: int, end: int):
     return np.asarray(t, dtype=np.float32)[..., begin:end]
 
 
+def _needs_grad(*xs) -> bool:
+    return torch.is_grad_enabled() and any(isinstance(x, torch.Tensor) and x.requires_grad for x in xs)
+
+
 def _broadcast_rows(y, t, event: int, width: int):
     """Bring ``y (..., event)`` and ``t (..., width)`` to 2-D row form for the kernel.
 
@@ -99,7 +103,10 @@ class MultivariateNormalDiag:
         if not self._trainable:
             B = max(y.shape[0], int(np.prod(self.batch_shape)) if len(self.batch_shape) else 1)
             y = y.expand(B, d) if y.shape[0] == 1 and B > 1 else y
-        lp, _ = ops.chain_log_prob(y, t, (), d, self._trainable)
+        if _needs_grad(y, t):
+            lp = ops.log_prob(y, t, (), d, self._trainable)
+        else:
+            lp, _ = ops.chain_log_prob(y, t, (), d, self._trainable)
         return lp if bshape is None else lp.reshape(bshape)
 
     def prob(self, x):
@@ -138,7 +145,10 @@ class FlowDistribution:
         ``-sum(log std)`` Jacobian correction (``BaseEstimator.py:85-86``)."""
         P = _shape(self._t)[-1]
         yy, tt, bshape = _broadcast_rows(y, self._t, self._n_dims, P)
-        lp, _ = ops.chain_log_prob(yy, tt, self._flow_types, self._n_dims, self._trainable, y_mean, y_std)
+        if _needs_grad(yy, tt):  # training: differentiable through the fused backward kernel
+            lp = ops.log_prob(yy, tt, self._flow_types, self._n_dims, self._trainable, y_mean, y_std)
+        else:
+            lp, _ = ops.chain_log_prob(yy, tt, self._flow_types, self._n_dims, self._trainable, y_mean, y_std)
         if bshape is not None:
             return lp.reshape(bshape)
         if len(self.batch_shape) == 0 and _shape(y) and len(_shape(y)) == 1:

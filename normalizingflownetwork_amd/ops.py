@@ -130,6 +130,95 @@ def chain_log_prob(
     return out, osum
 
 
+def chain_log_prob_grad(
+    y,
+    t,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+    g_out=None,
+    want_logp: bool = False,
+    want_grad_t: bool = True,
+    want_grad_y: bool = True,
+):
+    """Fused backward (one kernel): per sample ``dL/dt`` (B, P) and ``dL/dy`` (B, d) for
+    ``L = sum_b g_out[b] * log_prob_b`` (``g_out`` None => ones), optionally ``log_prob``.
+
+    What Keras autodiff computes through the reference's log_prob when it trains
+    (``BaseEstimator.py:19-31, 55-59``).  A broadcast input (batch 1) still gets
+    one gradient row per sample.  Returns ``(log_prob | None, grad_t | None, grad_y | None)``."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    y = _prep_2d(y, n_dims, "y", dev)
+    t = _prep_2d(t, P, "t", dev) if P > 0 else torch.zeros((1, 1), dtype=torch.float32, device=dev)
+    B = max(y.shape[0], t.shape[0] if P > 0 else 1)
+    assert y.shape[0] in (1, B) and (P == 0 or t.shape[0] in (1, B)), "incompatible batch sizes"
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+        assert ym.numel() == n_dims and ys.numel() == n_dims
+    g = None
+    if g_out is not None:
+        g = as_device_f32(g_out, dev).reshape(-1).contiguous()
+        assert g.numel() == B, f"g_out must have {B} elements"
+    lp = torch.empty((B,), dtype=torch.float32, device=dev) if want_logp else None
+    gt = torch.empty((B, P), dtype=torch.float32, device=dev) if (want_grad_t and P > 0) else None
+    gy = torch.empty((B, n_dims), dtype=torch.float32, device=dev) if want_grad_y else None
+    ids, k = flow_ids(flow_types)
+    rc = _lib.load().nfn_chain_logprob_grad_f32(
+        _ptr(y), _row_stride(y), _ptr(t), _row_stride(t) if P > 0 else 0, B, int(n_dims),
+        ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys), _ptr(g),
+        _ptr(lp), _ptr(gt), P if gt is not None else 0, _ptr(gy), _stream(),
+    )
+    _lib.check(rc, "nfn_chain_logprob_grad_f32")
+    if want_grad_t and gt is None:
+        gt = torch.empty((B, 0), dtype=torch.float32, device=dev)
+    return lp, gt, gy
+
+
+class _ChainLogProb(torch.autograd.Function):
+    """``log_prob`` as a differentiable op: forward = the fused forward kernel,
+    backward = the fused backward kernel (the chain is recomputed there, nothing
+    but the inputs is saved)."""
+
+    @staticmethod
+    def forward(ctx, y, t, flow_types, n_dims, trainable_base, y_mean, y_std):
+        out, _ = chain_log_prob(y, t, flow_types, n_dims, trainable_base, y_mean, y_std)
+        ctx.save_for_backward(y, t)
+        ctx.meta = (tuple(flow_types), int(n_dims), bool(trainable_base), y_mean, y_std)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, t = ctx.saved_tensors
+        flow_types, n_dims, trainable_base, y_mean, y_std = ctx.meta
+        need_y, need_t = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        _, gt, gy = chain_log_prob_grad(y, t, flow_types, n_dims, trainable_base, y_mean, y_std,
+                                        g_out=g.contiguous(), want_grad_t=need_t, want_grad_y=need_y)
+        B = g.shape[0]
+        if need_y and y.shape[0] == 1 and B > 1:
+            gy = gy.sum(0, keepdim=True)
+        if need_t and t.shape[0] == 1 and B > 1:
+            gt = gt.sum(0, keepdim=True)
+        return (gy if need_y else None), (gt if need_t else None), None, None, None, None, None
+
+
+def log_prob(y, t, flow_types: Sequence[str], n_dims: int, trainable_base: bool, y_mean=None, y_std=None):
+    """Differentiable fused ``log_prob`` (B,): gradients w.r.t. ``t`` and ``y`` flow
+    through ``torch.autograd`` via the fused backward kernel."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    y = _prep_2d(y, n_dims, "y", dev)
+    t = _prep_2d(t, P, "t", dev) if P > 0 else torch.zeros((1, 1), dtype=torch.float32, device=dev)
+    if y_mean is not None:
+        y_mean = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        y_std = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    return _ChainLogProb.apply(y, t, tuple(flow_types), int(n_dims), bool(trainable_base), y_mean, y_std)
+
+
 def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, want_ldj: bool = True):
     """One bijector: ``(forward(z), forward_log_det_jacobian(z))`` (either may be None)."""
     dev = _device()
@@ -258,3 +347,35 @@ class ChainLauncher:
         if rc != 0:
             _lib.check(rc, "nfn_reduce_partials_f64")
         return self.sum
+
+
+class GradLauncher:
+    """Pre-bound fused-backward launch over fixed device buffers (the training-step
+    benchmark): ``launch()`` writes ``grad_t`` (B, P) and ``grad_y`` (B, d) for the
+    upstream gradient ``g_out`` (B,) — one C-ABI call."""
+
+    def __init__(self, y: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
+                 trainable_base: bool, g_out: Optional[torch.Tensor] = None, write_logp: bool = False):
+        self.lib = _lib.load()
+        dev = y.device
+        self.n_dims = int(n_dims)
+        self.P = total_param_size(flow_types, n_dims, trainable_base)
+        assert y.dim() == 2 and y.shape[1] == n_dims and y.stride(1) == 1
+        assert t.dim() == 2 and t.shape[1] == self.P and t.stride(1) == 1
+        self.B = max(int(y.shape[0]), int(t.shape[0]))
+        assert g_out is None or (g_out.numel() == self.B and g_out.is_contiguous())
+        self.y, self.t, self.g_out = y, t, g_out
+        self.logp = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_logp else None
+        self.grad_t = torch.empty((self.B, self.P), dtype=torch.float32, device=dev)
+        self.grad_y = torch.empty((self.B, self.n_dims), dtype=torch.float32, device=dev)
+        self._ids, self._k = flow_ids(flow_types)
+        self._args = (
+            _ptr(y), _row_stride(y), _ptr(t), _row_stride(t), self.B, self.n_dims,
+            ctypes.cast(self._ids, ctypes.c_void_p), self._k, int(bool(trainable_base)), None, None,
+            _ptr(g_out), _ptr(self.logp), _ptr(self.grad_t), self.P, _ptr(self.grad_y),
+        )
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self.lib.nfn_chain_logprob_grad_f32(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_chain_logprob_grad_f32")

@@ -1,0 +1,167 @@
+"""Fused backward on the GPU against the autodiff oracle
+(oracle/nfn_grad_oracle.py, itself pinned by finite differences of the fp64
+forward oracle in tests/test_grad_oracle.py).
+
+Tolerance (per element, written here and in the oracle): ``grad_tolerance`` =
+max(2e-5 * max(1, |g64|, rowmax|g64| / 64), 8 * dev32), where dev32 is the largest
+deviation of the same autodiff restatement run in fp32 (the reference's own
+precision) at the inputs and at three 1-ulp perturbations of them
+(``oracle.nfn_grad_oracle.fp32_spread``)."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import CHAIN_FIXTURES, load_golden
+from oracle import nfn_grad_oracle as G
+
+pytestmark = pytest.mark.gpu
+
+NROWS = 1024  # oracle rows per fixture (autodiff on the CPU)
+
+
+def _grads_ref(y, t, ft, d, tr, ym=None, ys=None, g=None):
+    gt64, gy64, dev_t, dev_y = G.fp32_spread(y, t, ft, d, tr, ym, ys, g_out=g)
+    return gt64, dev_t, gy64, dev_y
+
+
+def _check(got, ref64, dev32, what, row_scale=True):
+    got = np.asarray(got, np.float64)
+    assert got.shape == ref64.shape, (what, got.shape, ref64.shape)
+    if got.size == 0:
+        return
+    bound = G.grad_tolerance(ref64, dev32, row_scale=row_scale)
+    err = np.abs(got - ref64)
+    finite = np.isfinite(ref64)
+    assert np.array_equal(np.isfinite(got), finite), f"{what}: non-finite pattern differs"
+    bad = finite & ~(err <= bound)
+    if bad.any():
+        i = np.argwhere(bad)[0]
+        raise AssertionError(f"{what}: {bad.sum()} elements out of tolerance; first {tuple(i)}: "
+                             f"got {got[tuple(i)]!r} ref64 {ref64[tuple(i)]!r} bound {bound[tuple(i)]!r}; "
+                             f"max err/bound {np.max(err[finite] / bound[finite]):.3g}")
+
+
+def _run(gpu, y, t, ft, d, tr, ym=None, ys=None, g=None):
+    from normalizingflownetwork_amd import ops
+
+    lp, gt, gy = ops.chain_log_prob_grad(torch.from_numpy(np.ascontiguousarray(y, np.float32)).to(gpu),
+                                         torch.from_numpy(np.ascontiguousarray(t, np.float32)).to(gpu), ft, d, tr,
+                                         ym, ys, None if g is None else torch.from_numpy(g).to(gpu), want_logp=True)
+    return lp.cpu().numpy(), gt.cpu().numpy(), gy.cpu().numpy()
+
+
+@pytest.fixture(params=["fast", "precise"])
+def math_mode(request, gpu):
+    from normalizingflownetwork_amd import ops
+
+    prev = ops.set_math_mode(request.param)
+    yield request.param
+    ops.set_math_mode(prev)
+
+
+@pytest.mark.parametrize("name", CHAIN_FIXTURES)
+def test_grad_fixture_vs_oracle(gpu, math_mode, name):
+    fx = load_golden(name)
+    ft, d, tr = fx["flow_types"], fx["d"], bool(fx["trainable"])
+    y, t = fx["y"][:NROWS], fx["t"][:NROWS]
+    gt64, dt32, gy64, dy32 = _grads_ref(y, t, ft, d, tr)
+    lp, gt, gy = _run(gpu, y, t, ft, d, tr)
+    B = max(len(y), len(t))
+    _check(gt, gt64, dt32, f"{name} d/dt [{math_mode}]")
+    _check(gy, gy64, dy32, f"{name} d/dy [{math_mode}]")
+    # the backward's own log_prob equals the forward oracle
+    from oracle import nfn_oracle as O
+
+    ref = fx["ref64"][:B]
+    bound = O.tolerance_bound(ref, fx["ref32"][:B])
+    ok = np.isfinite(ref)
+    assert np.all(np.abs(lp[ok] - ref[ok]) <= bound[ok]), name
+
+
+@pytest.mark.parametrize("ft,d", [(("planar", "radial") * 5, 1), (("affine", "planar", "radial"), 3),
+                                  (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8)])
+def test_grad_normalized_and_upstream(gpu, math_mode, ft, d):
+    rng = np.random.default_rng(5)
+    from oracle import nfn_oracle as O
+
+    P = O.total_param_size(ft, d, True)
+    B = 777  # ragged: not a multiple of the 64-row tile
+    y = rng.standard_normal((B, d)).astype(np.float32) * 2 + 0.5
+    t = rng.standard_normal((B, P)).astype(np.float32)
+    ym = np.linspace(0.2, 0.6, d).astype(np.float32)
+    ys = np.linspace(1.5, 2.5, d).astype(np.float32)
+    g = rng.standard_normal(B).astype(np.float32)
+    gt64, dt32, gy64, dy32 = _grads_ref(y, t, ft, d, True, ym, ys, g)
+    _, gt, gy = _run(gpu, y, t, ft, d, True, ym, ys, g)
+    _check(gt, gt64, dt32, f"{ft} d/dt normalized+g")
+    _check(gy, gy64, dy32, f"{ft} d/dy normalized+g")
+
+
+def test_grad_broadcast_inputs(gpu):
+    from normalizingflownetwork_amd import ops
+    from oracle import nfn_oracle as O
+
+    ft, d = ("planar", "radial", "affine"), 2
+    P = O.total_param_size(ft, d, True)
+    rng = np.random.default_rng(9)
+    y1 = rng.standard_normal((1, d)).astype(np.float32)
+    t = rng.standard_normal((300, P)).astype(np.float32)
+    gt64, dt32, gy64, dy32 = _grads_ref(y1, t, ft, d, True)
+    _, gt, gy = _run(gpu, y1, t, ft, d, True)
+    _check(gt, gt64, dt32, "y-broadcast d/dt")
+    _check(gy, gy64, dy32, "y-broadcast d/dy")
+    y = rng.standard_normal((300, d)).astype(np.float32)
+    t1 = t[:1]
+    gt64, dt32, gy64, dy32 = _grads_ref(y, t1, ft, d, True)
+    _, gt, gy = _run(gpu, y, t1, ft, d, True)
+    _check(gt, gt64, dt32, "t-broadcast d/dt")
+    _check(gy, gy64, dy32, "t-broadcast d/dy")
+    # strided t (a column slice of a wider buffer) and a strided grad_t buffer
+    wide = torch.from_numpy(np.concatenate([t, np.zeros((300, 3), np.float32)], 1)).to(gpu)
+    _, gts, _ = ops.chain_log_prob_grad(torch.from_numpy(y).to(gpu), wide[:, :P], ft, d, True)
+    _, gtc, _ = ops.chain_log_prob_grad(torch.from_numpy(y).to(gpu), torch.from_numpy(t).to(gpu), ft, d, True)
+    assert torch.equal(gts, gtc)
+
+
+def test_autograd_function_matches_kernel(gpu):
+    from normalizingflownetwork_amd import ops
+    from oracle import nfn_oracle as O
+
+    ft, d = ("planar", "radial") * 2, 1
+    P = O.total_param_size(ft, d, True)
+    rng = np.random.default_rng(2)
+    y = torch.from_numpy(rng.standard_normal((500, d)).astype(np.float32)).to(gpu).requires_grad_(True)
+    t = torch.from_numpy(rng.standard_normal((500, P)).astype(np.float32)).to(gpu).requires_grad_(True)
+    w = torch.linspace(-1, 1, 500, device=gpu)
+    lp = ops.log_prob(y, t, ft, d, True)
+    (lp * w).sum().backward()
+    _, gt, gy = ops.chain_log_prob_grad(y.detach(), t.detach(), ft, d, True, g_out=w)
+    assert torch.equal(t.grad, gt) and torch.equal(y.grad, gy)
+    # broadcast y through autograd reduces over the batch
+    y1 = y.detach()[:1].clone().requires_grad_(True)
+    ops.log_prob(y1, t.detach(), ft, d, True).sum().backward()
+    _, _, gyb = ops.chain_log_prob_grad(y1.detach(), t.detach(), ft, d, True)
+    torch.testing.assert_close(y1.grad, gyb.sum(0, keepdim=True), rtol=1e-5, atol=1e-4)
+
+
+def test_grad_full_size_c2_sampled(gpu):
+    """C2 at full size (2^24): every gradient finite where log_prob is, and a
+    random sample of rows matches the oracle."""
+    from normalizingflownetwork_amd import ops
+    from oracle import nfn_oracle as O
+
+    ft, d = ("planar", "radial") * 5, 1
+    P = O.total_param_size(ft, d, True)
+    B = 1 << 24
+    gen = torch.Generator(device=gpu).manual_seed(22)
+    y = torch.randn((B, d), generator=gen, device=gpu)
+    t = torch.randn((B, P), generator=gen, device=gpu)
+    lp, gt, gy = ops.chain_log_prob_grad(y, t, ft, d, True, want_logp=True)
+    fin = torch.isfinite(lp)
+    assert torch.isfinite(gt[fin]).all() and torch.isfinite(gy[fin]).all()
+    idx = torch.randperm(B, generator=torch.Generator().manual_seed(1))[:2048].to(gpu)
+    ys, ts = y[idx].cpu().numpy(), t[idx].cpu().numpy()
+    gt64, dt32, gy64, dy32 = _grads_ref(ys, ts, ft, d, True)
+    _check(gt[idx].cpu().numpy(), gt64, dt32, "C2 sampled d/dt")
+    _check(gy[idx].cpu().numpy(), gy64, dy32, "C2 sampled d/dy")

@@ -55,6 +55,11 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o w -- \
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    grad) run bench_grad_c2 300 python bench.py --mode grad --steps 20 --warmup 5 --cpu-seconds 8 ;;
+    grad_c3) run bench_grad_c3 300 python bench.py --mode grad --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof_grad)
+      { cd /tmp; run rocprof_grad 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_grad" -o grad -- \
+        python3 "$ROOT/bench.py" --mode grad --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
     debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
     mem) run mem 300 python tools/microbench.py mem ;;
