@@ -9,8 +9,9 @@ The x -> t network (the reference's Keras Dense stack) is not on the hot path
 produce ``t``.  Everything from ``t`` to the density / score runs in the fused
 HIP kernels: the y normalisation ``(y - mu)/sigma``, the whole flow chain, the
 base density, the ``-sum(log sigma)`` correction and (for ``score``) the fp64
-batch sum.  Training (``fit``) is out of scope for this round — the reference
-trains with Keras autodiff; the fused backward is the next row.
+batch sum.  ``fit`` trains on the GPU: torch autograd through the MLP and the
+fused backward kernel through the flow chain; the Bayesian
+estimator's variational training (KL term) is not mirrored.
 """
 
 from __future__ import annotations
@@ -79,6 +80,7 @@ class BaseEstimator:
         self.activation = activation
         self.random_seed = random_seed
         self.noise_fn_type, self.noise_scale_factor = noise_reg
+        self.x_noise_std = self.y_noise_std = 0.0  # set by fit (BaseEstimator.py:9-10, 33-41)
         self.x_mean = self.x_std = None
         self.y_mean = np.zeros((self.n_dims,), np.float32)
         self.y_std = np.ones((self.n_dims,), np.float32)
@@ -147,10 +149,78 @@ class BaseEstimator:
         s = output.log_prob_sum(y_data, self.y_mean, self.y_std)
         return float(s.item()) / int(y_data.shape[0])
 
-    def fit(self, *args, **kwargs):
-        raise NotImplementedError(
-            "training is out of scope for the log_prob hot path (SURVEY.md §2); the fused backward is next (§8(f))"
-        )
+    def _assign_noise_regularisation(self, n_dims: int, n_datapoints: int):
+        """``BaseEstimator.py:33-41``."""
+        assert self.noise_fn_type in ["rule_of_thumb", "fixed_rate"]
+        if self.noise_fn_type == "rule_of_thumb":
+            std = self.noise_scale_factor * (n_datapoints + 1) ** (-1 / (4 + n_dims))
+        else:
+            std = self.noise_scale_factor
+        self.x_noise_std = self.y_noise_std = float(std)
+
+    def fit(self, x, y, batch_size=None, epochs=None, verbose=1, shuffle=True, **kwargs):
+        """Maximum-likelihood training on the GPU: ``BaseEstimator.fit`` (``BaseEstimator.py:19-31``)
+        with the model compiled as in ``MaximumLikelihoodNNEstimator.py:33-35`` —
+        Adam(learning_rate), loss = mean over the batch of ``-log_prob(y_circ + noise | t)
+        + sum(log y_std)`` (``BaseEstimator.py:55-67``), Keras defaults ``batch_size=32``,
+        ``epochs=1``, per-epoch shuffling, GaussianNoise on the normalised x and y while
+        training, and TerminateOnNaN.  ``t = MLP(x)`` runs in torch; ``log_prob`` and its
+        gradient w.r.t. ``t`` run in the fused HIP kernels (``nfn_chain_logprob_f32`` /
+        ``nfn_chain_logprob_grad_f32``).  Returns ``{"loss": [per-epoch mean loss]}``."""
+        x = np.asarray(x, np.float32)
+        y = np.asarray(y, np.float32)
+        assert len(x.shape) == len(y.shape) == 2, "Please pass a matrix not a vector"
+        self._assign_data_normalization(x, y)
+        self._assign_noise_regularisation(n_dims=x.shape[1] + y.shape[1], n_datapoints=x.shape[0])
+        if self._mlp is None:
+            self._build(int(x.shape[1]))
+        dev = ops._device()
+        self._mlp.to(dev)
+        params = [p.detach().requires_grad_(True) for p in self._mlp.weights + self._mlp.biases]
+        nw = len(self._mlp.weights)
+        self._mlp.weights, self._mlp.biases = params[:nw], params[nw:]
+        lr = getattr(self, "learning_rate", 3e-3)
+        opt = torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-7)  # Keras Adam defaults
+        batch_size = 32 if batch_size is None else int(batch_size)
+        epochs = 1 if epochs is None else int(epochs)
+        X = torch.from_numpy(x).to(dev)
+        Y = torch.from_numpy(y).to(dev)
+        xm, xs = (torch.as_tensor(v, dtype=torch.float32, device=dev) for v in (self.x_mean, self.x_std))
+        ym, ys = (torch.as_tensor(v, dtype=torch.float32, device=dev) for v in (self.y_mean, self.y_std))
+        sum_log_ys = torch.log(ys).sum()
+        gen = torch.Generator(device=dev).manual_seed(int(self.random_seed))
+        dl = self.dist_layer
+        n = X.shape[0]
+        history = {"loss": []}
+        try:
+            for _ in range(epochs):
+                perm = torch.randperm(n, generator=gen, device=dev) if shuffle else torch.arange(n, device=dev)
+                acc = torch.zeros((), dtype=torch.float64, device=dev)
+                for i in range(0, n, batch_size):
+                    idx = perm[i:i + batch_size]
+                    xn = (X[idx] - xm) / (xs + 1e-8)
+                    if self.x_noise_std > 0:
+                        xn = xn + self.x_noise_std * torch.randn(xn.shape, generator=gen, device=dev)
+                    yc = (Y[idx] - ym) / ys
+                    if self.y_noise_std > 0:
+                        yc = yc + self.y_noise_std * torch.randn(yc.shape, generator=gen, device=dev)
+                    t = self._mlp(xn)
+                    lp = ops.log_prob(yc, t, dl.flow_types, self.n_dims, dl.trainable_base_dist)
+                    loss = -lp.mean() + sum_log_ys
+                    opt.zero_grad(set_to_none=True)
+                    loss.backward()
+                    opt.step()
+                    acc += loss.detach().double() * idx.numel()
+                ep_loss = float(acc.item()) / n
+                history["loss"].append(ep_loss)
+                if verbose:
+                    print(f"epoch {len(history['loss'])}/{epochs} loss {ep_loss:.6f}", flush=True)
+                if not np.isfinite(ep_loss):  # tf.keras.callbacks.TerminateOnNaN
+                    break
+        finally:
+            self._mlp.weights = [p.detach() for p in self._mlp.weights]
+            self._mlp.biases = [p.detach() for p in self._mlp.biases]
+        return history
 
 
 class NormalizingFlowNetwork(BaseEstimator):

@@ -112,3 +112,18 @@ def test_shard_bounds_partition(n, world):
         assert b == c and b >= a
     sizes = [b - a for a, b in spans]
     assert max(sizes) - min(sizes) <= 1
+
+
+def test_noise_regularisation_values():
+    """BaseEstimator._assign_noise_regularisation (BaseEstimator.py:33-41)."""
+    from normalizingflownetwork_amd import NormalizingFlowNetwork
+
+    m = NormalizingFlowNetwork(1, n_flows=1, noise_reg=("rule_of_thumb", 0.1))
+    m._assign_noise_regularisation(n_dims=2, n_datapoints=300)
+    assert m.x_noise_std == m.y_noise_std == pytest.approx(0.1 * 301 ** (-1 / 6))
+    m = NormalizingFlowNetwork(1, n_flows=1, noise_reg=("fixed_rate", 3.0))
+    m._assign_noise_regularisation(n_dims=2, n_datapoints=300)
+    assert m.x_noise_std == 3.0
+    m = NormalizingFlowNetwork(1, n_flows=1, noise_reg=("bogus", 3.0))
+    with pytest.raises(AssertionError):
+        m._assign_noise_regularisation(n_dims=2, n_datapoints=300)

@@ -1,0 +1,139 @@
+"""Training on the GPU through the fused backward: the
+reference's estimator tests that call ``fit`` (tests/test_ml_estimator.py,
+tests/test_noise_reg.py), restated with numpy data of the same distributions, and
+an end-to-end check of the MLP weight gradients against the autodiff oracle."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nfn_grad_oracle as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _nfn(*args, **kw):
+    from normalizingflownetwork_amd import NormalizingFlowNetwork
+
+    return NormalizingFlowNetwork(*args, **kw)
+
+
+def test_ml_dims_after_fit(gpu):
+    """tests/test_ml_estimator.py:19-40, 86-101 (NFN rows)."""
+    x = np.linspace(-1, 1, 10).reshape((10, 1))
+    m = _nfn(1, n_flows=1, hidden_sizes=(2, 2), trainable_base_dist=False)
+    m.fit(x, x, epochs=1, verbose=0)
+    out = m(x)
+    assert out.event_shape == [1] and out.batch_shape == [10]
+    assert tuple(out.log_prob([[0.0]]).shape) == (10,)
+    x3 = np.linspace([[-1]] * 3, [[1]] * 3, 10).reshape((10, 3))
+    m3 = _nfn(3, n_flows=1, hidden_sizes=(2, 2), trainable_base_dist=True)
+    m3.fit(x3, x3, epochs=1, verbose=0)
+    out3 = m3(x3)
+    assert out3.event_shape == [3] and out3.batch_shape == [10]
+    assert tuple(out3.log_prob([[0.0] * 3]).shape) == (10,)
+
+
+def test_fit_rejects_vectors(gpu):
+    m = _nfn(1, n_flows=1)
+    with pytest.raises(AssertionError):
+        m.fit(np.zeros(10), np.zeros(10))
+
+
+def test_weight_gradients_match_autodiff_oracle(gpu):
+    """One training loss: MLP weight gradients with the fused backward kernel vs
+    fp64 autodiff of the oracle's op sequence through the same MLP."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d = ("planar", "radial", "radial"), 1
+    m = _nfn(d, flow_types=ft, hidden_sizes=(10, 10), trainable_base_dist=True, n_dims_x=1)
+    rng = np.random.default_rng(4)
+    x = rng.standard_normal((256, 1)).astype(np.float32)
+    y = (np.sin(2 * x) + 0.3 * rng.standard_normal((256, 1))).astype(np.float32)
+    m._mlp.to(gpu)
+    ws = [w.detach().requires_grad_(True) for w in m._mlp.weights + m._mlp.biases]
+    nw = len(m._mlp.weights)
+
+    def mlp(xx, params):
+        h = xx
+        for i in range(nw):
+            h = h @ params[i] + params[nw + i]
+            if i < nw - 1:
+                h = torch.relu(h)
+        return h
+
+    t = mlp(torch.from_numpy(x).to(gpu), ws)
+    loss = -ops.log_prob(torch.from_numpy(y).to(gpu), t, ft, d, True).mean()
+    loss.backward()
+    got = [w.grad.double().cpu() for w in ws]
+    ws64 = [w.detach().double().cpu().requires_grad_(True) for w in ws]
+    t64 = mlp(torch.from_numpy(x).double(), ws64)
+    lp64 = G.chain_log_prob_torch(torch.from_numpy(y).double(), t64, ft, d, True)
+    (-lp64.mean()).backward()
+    for g, w in zip(got, ws64):
+        torch.testing.assert_close(g, w.grad, rtol=2e-4, atol=2e-5)
+
+
+def _sinusoid(n, rng):
+    x = np.linspace(-3, 3, n, dtype=np.float32).reshape((n, 1))
+    y = (5 * np.sin(2 * x) + np.abs(x) * rng.standard_normal((n, 1))).astype(np.float32)
+    return x, y
+
+
+def _sinusoid_pdf(x, y):
+    s = np.abs(x)
+    return np.exp(-0.5 * ((y - 5 * np.sin(2 * x)) / s) ** 2) / (np.sqrt(2 * np.pi) * s)
+
+
+def test_ml_nf_fitting_sinusoid(gpu):
+    """tests/test_ml_estimator.py:43-59, 104-107: NFN(1, n_flows=3, (10, 10)) fitted
+    800 epochs on 400 heteroscedastic sinusoid points; mean |pdf - true pdf| < 0.45."""
+    rng = np.random.default_rng(22)
+    m = _nfn(1, n_flows=3, hidden_sizes=(10, 10), trainable_base_dist=True)
+    x, y = _sinusoid(400, rng)
+    hist = m.fit(x, y, epochs=800, verbose=0)
+    assert hist["loss"][-1] < hist["loss"][0]
+    xt, yt = _sinusoid(1000, rng)
+    pdf = m.pdf(xt, yt).cpu().numpy().reshape(-1)
+    score = np.sum(np.abs(pdf - _sinusoid_pdf(xt, yt).reshape(-1))) / 1000.0
+    assert score < 0.45, score
+
+
+def test_ml_nf_fitting_bimodal(gpu):
+    """tests/test_ml_estimator.py:62-83, 108: equal mixture of N(3, 0.5) and N(-3, 0.5)
+    independent of x; mean |pdf - true pdf| < 0.1012."""
+    rng = np.random.default_rng(22)
+
+    def data(n):
+        x = np.linspace(-3, 3, n, dtype=np.float32).reshape((n, 1))
+        c = rng.integers(0, 2, (n, 1))
+        y = (np.where(c == 0, 3.0, -3.0) + 0.5 * rng.standard_normal((n, 1))).astype(np.float32)
+        return x, y
+
+    def true_pdf(y):
+        n = lambda mu: np.exp(-0.5 * ((y - mu) / 0.5) ** 2) / (np.sqrt(2 * np.pi) * 0.5)  # noqa: E731
+        return 0.5 * n(3.0) + 0.5 * n(-3.0)
+
+    m = _nfn(1, n_flows=3, hidden_sizes=(10, 10), trainable_base_dist=True)
+    x, y = data(400)
+    m.fit(x, y, epochs=800, verbose=0)
+    xt, yt = data(1000)
+    score = np.sum(np.abs(m.pdf(xt, yt).cpu().numpy().reshape(-1) - true_pdf(yt).reshape(-1))) / 1000.0
+    assert score < 0.1012, score
+
+
+def test_noise_off_at_evaluation(gpu):
+    """tests/test_noise_reg.py:13-33: with heavy noise regularisation the fitted
+    model's pdf is deterministic at evaluation (noise only while training), and a
+    lightly regularised model scores higher than the over-regularised one."""
+    rng = np.random.default_rng(22)
+    x, y = _sinusoid(300, rng)
+    heavy = _nfn(1, n_flows=2, hidden_sizes=(16, 16), noise_reg=("fixed_rate", 3.0), trainable_base_dist=True)
+    heavy.fit(x, y, epochs=700, verbose=0)
+    xt, yt = _sinusoid(300, rng)
+    p1 = heavy.pdf(xt, yt).cpu().numpy()
+    p2 = heavy.pdf(xt, yt).cpu().numpy()
+    assert np.array_equal(p1, p2)
+    light = _nfn(1, n_flows=2, hidden_sizes=(16, 16), noise_reg=("rule_of_thumb", 0.1), trainable_base_dist=True)
+    light.fit(x, y, epochs=700, verbose=0)
+    assert light.pdf(xt, yt).sum().item() / 700.0 > p1.sum() / 700.0
