@@ -19,6 +19,7 @@ OBJ_DIR = os.path.join(PKG_DIR, "_obj")
 OUT = os.path.join(PKG_DIR, "libnfn_hip.so")
 ARCH = os.environ.get("NFN_OFFLOAD_ARCH", "gfx950")
 HEADERS = [os.path.join(CSRC, "nfn_device.h"), os.path.join(CSRC, "nfn_launch.h"),
+           os.path.join(CSRC, "nfn_grad_device.h"),
            os.path.join(REPO_DIR, "include", "nfn.h")]
 # (object name, source, extra flags)
 UNITS = [
@@ -30,6 +31,8 @@ UNITS = [
     ("tile", "nfn_tile.hip", []),
     ("misc", "nfn_misc.hip", []),
     ("grad", "nfn_grad.hip", []),
+    ("grad_group_fast", "nfn_grad_group.hip", ["-DNFN_FAST=1"]),
+    ("grad_group_precise", "nfn_grad_group.hip", ["-DNFN_FAST=0"]),
     ("comm", "nfn_comm.hip", []),
 ]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")

@@ -314,8 +314,40 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   ga.gt_rowstride = grad_t ? gt_rowstride : 0;
   ga.gt_vec4 = ((P & 3) == 0) && ((gt_rowstride & 3) == 0) && ((reinterpret_cast<uintptr_t>(grad_t) & 15) == 0);
   ga.rows = R;
-  launch_grad(use_fast_math(), dm_for(d), ga, dim3((unsigned)nblk), (size_t)R * row_bytes,
-              reinterpret_cast<hipStream_t>(stream));
+  // diagnostics (microbenchmarks): memory-only / compute-only timing
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int Q = P >> 2;
+  const int dm = dm_for(d);
+  const size_t slot = (size_t)(64 * S + a.prog.K * d * 64) * sizeof(float);
+  const bool wave_ok = a.vec4 && t_rowstride != 0 && P > 0 && (Q & (Q - 1)) == 0 && Q <= 16 && dm <= 2 &&
+                       (!grad_t || ga.gt_vec4) && slot <= (size_t)40 * 1024 && env_int("NFN_GRAD_WAVE", 1) != 0;
+  if (dm >= 4 && a.vec4 && t_rowstride != 0 && Q >= 1 && (!grad_t || ga.gt_vec4) &&
+      env_int("NFN_GRAD_GROUP", 1) != 0) {
+    int G = 4, DPL = 1;
+    group_shape(dm, 0, &G, &DPL);
+    const int Rg = 64 / G;
+    const int nv = (Q + G - 1) / G;  // float4 slots per lane: (R rows x Q) / 64
+    a.lds_stride = group_lds_stride(P, G);
+    const size_t gslot = (size_t)(Rg * a.lds_stride + a.prog.K * DPL * 64) * sizeof(float);
+    if (nv <= 16 && gslot <= (size_t)40 * 1024) {
+      a.ntiles = (B + Rg - 1) / Rg;
+      int64_t grid = 0;
+      const bool ok = use_fast_math() ? launch_grad_group_fast(G, DPL, nv, ga, 4 * gslot, s, &grid)
+                                      : launch_grad_group_precise(G, DPL, nv, ga, 4 * gslot, s, &grid);
+      if (ok) return check_hip("chain_grad_group_kernel launch");
+    }
+    a.lds_stride = S;
+  }
+  if (wave_ok) {
+    a.ntiles = (B + 63) / 64;
+    const int wpb = slot * 4 <= (size_t)80 * 1024 ? 4 : (slot * 2 <= (size_t)80 * 1024 ? 2 : 1);
+    int64_t grid = 0;
+    if (launch_grad_wave(use_fast_math(), dm, Q, ga, slot * wpb, wpb, s, &grid))
+      return check_hip("chain_grad_wave_kernel launch");
+  }
+  launch_grad(use_fast_math(), dm, ga, dim3((unsigned)nblk), (size_t)R * row_bytes, s);
   return check_hip("chain_grad_kernel launch");
 }
 

@@ -1,0 +1,534 @@
+// nfn_grad_device.h — closed-form adjoints of the flow chain,
+// shared by the backward kernels (nfn_grad.hip, nfn_grad_group.hip).
+//
+// `a` enters as d logp / d z_{k+1} and leaves as d logp / d z_k; `gl` is the
+// adjoint of every log-det term (the upstream gradient g_b); each flow overwrites
+// its own parameter block with d logp / d (its parameters).  What Keras autodiff
+// computes through PlanarFlow.py:43-80, RadialFlow.py:44-84, AffineFlow.py:4-9 and
+// DistributionLayers.py:280-294 when the reference trains.
+// Derivations: tests/analytic_grad.py (checked against autodiff in fp64).
+#pragma once
+
+#include "nfn_device.h"
+
+namespace nfn {
+
+template <bool FAST>
+__device__ __forceinline__ float f_sigmoid(float x) {
+  if constexpr (FAST) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x * kLog2e));
+  } else {
+    return 1.0f / (1.0f + expf(-x));
+  }
+}
+
+__device__ __forceinline__ float sign0(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+
+// Adjoints.  `a` enters as d logp / d z_{k+1} and leaves as d logp / d z_k;
+// `gl` is the adjoint of every log-det term (the upstream gradient g_b).
+// Derivations: tests/analytic_grad.py (checked against autodiff in fp64).
+
+// Planar: u_hat = u + c w / n, c = (-1 + softplus(w.u) + 1e-5) - w.u, n = |w|^2 + 1e-9,
+// f = z + u_hat tanh(w.z + b), ldj = log|1 + (1 - tanh^2) w.u_hat|.
+template <int DM, bool FAST>
+__device__ __forceinline__ void planar_bwd(const float (&z)[DM], float (&a)[DM], float* p, int d, float gl) {
+  float u[DM], w[DM];
+  float wtu = 0.0f, nw2 = 0.0f, s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      u[j] = p[j];
+      w[j] = p[d + j] + 1.0f;
+      wtu += w[j] * u[j];
+      nw2 += w[j] * w[j];
+      s += w[j] * z[j];
+    } else {
+      u[j] = 0.0f;
+      w[j] = 0.0f;
+    }
+  }
+  s += p[2 * d];
+  nw2 += 1e-9f;
+  const float m = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;  // = w . u_hat (the constraint)
+  const float c = m - wtu;
+  const float sg = f_sigmoid<FAST>(wtu);
+  const float cn = f_div_acc<FAST>(c, nw2);
+  // tanh and its derivative from E = e^{-2|s|}: 1 - tanh^2 = 4E / (1 + E)^2 keeps its
+  // relative accuracy where tanh saturates (1 - h*h would cancel to 0 or 1 ulp).
+  const float E = f_exp<FAST>(-2.0f * fabsf(s));
+  const float rE = f_div<FAST>(1.0f, 1.0f + E);
+  float h;
+  if constexpr (FAST)
+    h = copysignf((1.0f - E) * rE, s);
+  else
+    h = tanhf(s);
+  const float hp = 4.0f * E * rE * rE;
+  float uh[DM];
+  float ua = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    uh[j] = fmaf(cn, w[j], u[j]);
+    ua += uh[j] * a[j];
+  }
+  // w . u_hat = wtu + c |w|^2 / n = m - c * 1e-9 / n, without the d-term cancellation
+  const float q = m - cn * 1e-9f;
+  const float hpd = gl * f_div<FAST>(hp, 1.0f + hp * q);
+  const float Ss = hp * ua - 2.0f * q * h * hpd;
+  float G[DM];
+  float wG = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    G[j] = h * a[j] + hpd * w[j];
+    wG += w[j] * G[j];
+  }
+  const float wGn = f_div<FAST>(wG, nw2);
+  const float k1 = (sg - 1.0f) * wGn;
+  const float k2 = 2.0f * cn * wGn;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      // d = 1: G - (1 - sg) (wG/n) w = G (1e-9 + sg w^2) / n exactly (no cancellation
+      // when sg -> 0); for d > 1 the along-w cancellation is the reference's own.
+      p[j] = d == 1 ? G[j] * f_div<FAST>(fmaf(sg * w[j], w[j], 1e-9f), nw2) : G[j] + k1 * w[j];
+      p[d + j] = z[j] * Ss + hpd * uh[j] + cn * G[j] - k2 * w[j] + k1 * u[j];
+      a[j] = fmaf(w[j], Ss, a[j]);
+    }
+  }
+  p[2 * d] = Ss;
+}
+
+// Radial: alpha = softplus(0.3 a0 - 2), beta = softplus(0.1 b0 + log(e-1)) - 1,
+// h = 1/(alpha + |z-gamma|_1), f = z + alpha beta h (z - gamma),
+// ldj = (d-1) log(1 + ab h) + log(1 + ab alpha h^2)   (= the reference's
+// 1 + ab h + ab h' r with h' = -h^2).
+template <int DM, bool FAST>
+__device__ __forceinline__ void radial_bwd(const float (&z)[DM], float (&a)[DM], float* p, int d, float gl) {
+  const float xa = 0.3f * p[0] - 2.0f;
+  const float xb = 0.1f * p[1] + kLogExpm1One;
+  const float al = softplus_tf<FAST>(xa);
+  const float be = softplus_tf<FAST>(xb) - 1.0f;
+  float dz[DM];
+  float r = 0.0f, da = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    dz[j] = j < d ? z[j] - p[2 + j] : 0.0f;
+    r += fabsf(dz[j]);
+    da += dz[j] * a[j];
+  }
+  const float h = f_div<FAST>(1.0f, al + r);
+  const float hh = h * h;
+  const float ab = al * be;
+  const float A = 1.0f + ab * h;
+  const float rB = f_div<FAST>(1.0f, 1.0f + ab * al * hh);
+  const float dm1 = (float)(d - 1);
+  const float rA = d > 1 ? f_div<FAST>(dm1, A) : 0.0f;  // (d-1) / A
+  const float H = ab * da + gl * (ab * rA + 2.0f * ab * al * h * rB);
+  const float g_ab = h * da + gl * (h * rA + al * hh * rB);
+  const float g_al = be * g_ab + gl * ab * hh * rB - hh * H;
+  const float hH = hh * H;
+  const float abh = ab * h;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      const float sg = sign0(dz[j]);
+      p[2 + j] = hH * sg - abh * a[j];
+      a[j] = A * a[j] - hH * sg;
+    }
+  }
+  p[0] = 0.3f * f_sigmoid<FAST>(xa) * g_al;
+  p[1] = 0.1f * f_sigmoid<FAST>(xb) * al * g_ab;
+}
+
+// Affine: f = z * (1 + s) + shift, ldj = sum log|1 + s|.
+template <int DM, bool FAST>
+__device__ __forceinline__ void affine_bwd(const float (&z)[DM], float (&a)[DM], float* p, int d, float gl) {
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      const float sc = 1.0f + p[d + j];
+      p[j] = a[j];
+      p[d + j] = z[j] * a[j] + gl * f_div<FAST>(1.0f, sc);
+      a[j] *= sc;
+    }
+  }
+}
+
+// Base MVNDiag(loc = t[:d], scale = 1e-3 + softplus(log(e-1) + 0.1 t[d:2d])), or N(0, I).
+template <int DM, bool FAST>
+__device__ __forceinline__ void base_bwd(const float (&z)[DM], float (&a)[DM], float* p, int d, bool trainable,
+                                         float gl) {
+#pragma unroll
+  for (int j = 0; j < DM; ++j) {
+    if (j < d) {
+      if (trainable) {
+        const float xs = kLogExpm1One + 0.1f * p[d + j];
+        const float rs = f_div<FAST>(1.0f, 1e-3f + softplus_tf<FAST>(xs));
+        const float zz = (z[j] - p[j]) * rs;
+        const float gz = gl * zz * rs;
+        a[j] = -gz;
+        p[j] = gz;
+        p[d + j] = 0.1f * f_sigmoid<FAST>(xs) * gl * fmaf(zz, zz, -1.0f) * rs;
+      } else {
+        a[j] = -gl * z[j];
+      }
+    } else {
+      a[j] = 0.0f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// d = 1, fast math: scalar forms of the same adjoints with the transcendentals
+// shared (softplus and sigmoid from one exponential, one reciprocal of |w|^2).
+// ---------------------------------------------------------------------------
+
+// softplus(x) and sigmoid(x) from e = e^{-|x|}: sigmoid = 1/(1+e) (x >= 0) or e/(1+e).
+__device__ __forceinline__ void sp_sig1(float x, float& sp, float& sg) {
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+  const float r = __builtin_amdgcn_rcpf(1.0f + e);
+  sp = fmaf(__builtin_amdgcn_logf(1.0f + e), kLn2, fmaxf(x, 0.0f));
+  sg = x >= 0.0f ? r : e * r;
+}
+
+// z-only forward steps (the backward needs each flow's input, not its log-det).
+__device__ __forceinline__ void planar1_z(float& z, float u, float wraw, float b) {
+  const float w = wraw + 1.0f;
+  const float wtu = w * u;
+  const float coef = sp_fast1(wtu) - (wtu + (1.0f - 1e-5f));
+  const float uh = fmaf(coef, f_div_acc<true>(w, fmaf(w, w, 1e-9f)), u);
+  const float E = __builtin_amdgcn_exp2f(fmaf(w, z, b) * (2.0f * kLog2e));
+  z = fmaf(uh, 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f)), z);
+}
+
+__device__ __forceinline__ void radial1_z(float& z, float a0, float b0, float g) {
+  const float alpha = sp_fast1(fmaf(0.3f, a0, -2.0f));
+  const float ab = fmaf(alpha, sp_fast1(fmaf(0.1f, b0, kLogExpm1One)), -alpha);
+  const float dz = z - g;
+  z = fmaf(ab * __builtin_amdgcn_rcpf(alpha + fabsf(dz)), dz, z);
+}
+
+// (p0, p1, p2): the flow's parameters (already read); `p`: where its gradient goes.
+__device__ __forceinline__ void planar1_bwd(float z, float& a, float p0, float p1, float p2, float* p, float gl) {
+  const float u = p0;
+  const float w = p1 + 1.0f;
+  const float wtu = w * u;
+  float sp, sg;
+  sp_sig1(wtu, sp, sg);
+  const float m = (sp - 1.0f) + 1e-5f;
+  const float c = m - wtu;
+  const float nw2 = fmaf(w, w, 1e-9f);
+  const float rn = __builtin_amdgcn_rcpf(nw2);
+  const float q0 = c * rn;
+  const float cn = fmaf(fmaf(-nw2, q0, c), rn, q0);  // c / n, Newton-refined
+  const float uh = fmaf(cn, w, u);
+  const float s = fmaf(w, z, p2);
+  const float E = __builtin_amdgcn_exp2f(fabsf(s) * (-2.0f * kLog2e));
+  const float rE = __builtin_amdgcn_rcpf(1.0f + E);
+  const float h = copysignf((1.0f - E) * rE, s);
+  const float hp = 4.0f * E * rE * rE;
+  const float q = fmaf(-cn, 1e-9f, m);
+  const float hpd = gl * hp * __builtin_amdgcn_rcpf(fmaf(hp, q, 1.0f));
+  const float Ss = fmaf(hp, uh * a, -2.0f * q * h * hpd);
+  const float G = fmaf(h, a, hpd * w);
+  const float wGn = w * G * rn;
+  const float k1 = (sg - 1.0f) * wGn;
+  p[0] = G * (fmaf(sg * w, w, 1e-9f) * rn);
+  p[1] = fmaf(z, Ss, fmaf(hpd, uh, fmaf(cn, G, fmaf(-2.0f * cn * wGn, w, k1 * u))));
+  p[2] = Ss;
+  a = fmaf(w, Ss, a);
+}
+
+__device__ __forceinline__ void radial1_bwd(float z, float& a, float p0, float p1, float p2, float* p, float gl) {
+  const float xa = fmaf(0.3f, p0, -2.0f);
+  const float xb = fmaf(0.1f, p1, kLogExpm1One);
+  float al, sga, spb, sgb;
+  sp_sig1(xa, al, sga);
+  sp_sig1(xb, spb, sgb);
+  const float be = spb - 1.0f;
+  const float dz = z - p2;
+  const float h = __builtin_amdgcn_rcpf(al + fabsf(dz));
+  const float hh = h * h;
+  const float ab = fmaf(al, spb, -al);
+  const float rB = __builtin_amdgcn_rcpf(fmaf(ab * al, hh, 1.0f));
+  const float da = dz * a;
+  const float glr = gl * rB;
+  const float H = fmaf(ab, da, 2.0f * ab * al * h * glr);
+  const float g_ab = fmaf(h, da, al * hh * glr);
+  const float g_al = fmaf(be, g_ab, ab * hh * glr) - hh * H;
+  const float hH = hh * H;
+  const float sg = sign0(dz);
+  p[0] = 0.3f * sga * g_al;
+  p[1] = 0.1f * sgb * al * g_ab;
+  p[2] = fmaf(hH, sg, -ab * h * a);
+  a = fmaf(fmaf(ab, h, 1.0f), a, -hH * sg);
+}
+
+__device__ __forceinline__ void affine1_bwd(float z, float& a, float p0, float p1, float* p, float gl) {
+  (void)p0;
+  const float sc = 1.0f + p1;
+  p[0] = a;
+  p[1] = fmaf(z, a, gl * __builtin_amdgcn_rcpf(sc));
+  a *= sc;
+}
+
+__device__ __forceinline__ void flow1_bwd(int id, float z, float& a, const float (&pv)[3], float* p, float gl) {
+  if (id == NFN_FLOW_PLANAR)
+    planar1_bwd(z, a, pv[0], pv[1], pv[2], p, gl);
+  else if (id == NFN_FLOW_RADIAL)
+    radial1_bwd(z, a, pv[0], pv[1], pv[2], p, gl);
+  else
+    affine1_bwd(z, a, pv[0], pv[1], p, gl);
+}
+
+// d = 1, fast math, chains of <= 16 flows with the packed program (types 2 bits
+// per flow; offsets by scalar arithmetic: no scalar-memory loads inside the
+// loops, whose lgkmcnt(0) waits would drain the pipelined LDS reads).  Both
+// passes read the NEXT flow's parameters (and, in reverse, its input z) from LDS
+// before evaluating the current flow.
+__device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, int zs, uint32_t types, int K, int P,
+                                              bool trainable, float gl, bool want_lp, float& adj) {
+  float l2 = 0.0f;
+  int id = (int)(types & 3u);
+  int off = max(P - size1(id), 0);
+  float pc[3];
+  if (K > 0) read3c(pc, row, off);
+#pragma unroll 1
+  for (int k = 0; k < 16; ++k) {
+    if (k < K) {
+      const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
+      const int offn = max(off - size1(idn), 0);
+      float pn[3];
+      read3c(pn, row, offn);
+      zh[k * zs] = z;
+      if (want_lp) {
+        l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+      } else if (id == NFN_FLOW_PLANAR) {
+        planar1_z(z, pc[0], pc[1], pc[2]);
+      } else if (id == NFN_FLOW_RADIAL) {
+        radial1_z(z, pc[0], pc[1], pc[2]);
+      } else {
+        z = fmaf(z, 1.0f + pc[1], pc[0]);
+      }
+      id = idn;
+      off = offn;
+      pc[0] = pn[0];
+      pc[1] = pn[1];
+      pc[2] = pn[2];
+    }
+  }
+  const float lp = want_lp ? base1_fast(z, row, trainable) + l2 * kLn2 : 0.0f;
+  float a1;
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[1], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    a1 = -gz;
+    row[0] = gz;
+    row[1] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+  } else {
+    a1 = -gl * z;
+  }
+  // reverse: flow K-1's block follows the base, flow k-1's follows flow k's
+  int ob = trainable ? 2 : 0;
+  int ib = (int)((types >> (2 * (K - 1) & 31)) & 3u);
+  float pb[3] = {0.0f, 0.0f, 0.0f};
+  float zb = 0.0f;
+  if (K > 0) {
+    read3c(pb, row, ob);
+    zb = zh[(K - 1) * zs];
+  }
+#pragma unroll 1
+  for (int k = 15; k >= 0; --k) {
+    if (k < K) {
+      const int ip = (int)((types >> (2 * (k - 1) & 31)) & 3u);
+      const int op = min(ob + size1(ib), P - 1);  // k = 0: a harmless in-slot read
+      float pp[3];
+      read3c(pp, row, op);
+      const float zp = zh[max(k - 1, 0) * zs];
+      flow1_bwd(ib, zb, a1, pb, row + ob, gl);
+      ib = ip;
+      ob = op;
+      pb[0] = pp[0];
+      pb[1] = pp[1];
+      pb[2] = pp[2];
+      zb = zp;
+    }
+  }
+  adj = a1;
+  return lp;
+}
+
+
+// ---------------------------------------------------------------------------
+// Lane-group forms (d >= 4): a G-lane group owns one sample, lane j holds the
+// DPL dimensions j, j + G, ...; inner products are DPP group sums (gsum).
+// ---------------------------------------------------------------------------
+
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d, int j,
+                                              float gl) {
+  float u[DPL], w[DPL];
+  float swu = 0.0f, sww = 0.0f, swz = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const bool act = j + G * i < d;
+    u[i] = act ? p[j + G * i] : 0.0f;
+    w[i] = act ? p[d + j + G * i] + 1.0f : 0.0f;
+    swu += w[i] * u[i];
+    sww += w[i] * w[i];
+    swz += w[i] * z[i];
+  }
+  const float wtu = gsum<G>(swu);
+  const float nw2 = gsum<G>(sww) + 1e-9f;
+  const float s = gsum<G>(swz) + p[2 * d];
+  float sp, sg;
+  if constexpr (FAST) {
+    sp_sig1(wtu, sp, sg);
+  } else {
+    sp = softplus_tf<false>(wtu);
+    sg = f_sigmoid<false>(wtu);
+  }
+  const float m = (-1.0f + sp) + 1e-5f;
+  const float c = m - wtu;
+  const float cn = f_div_acc<FAST>(c, nw2);
+  const float E = f_exp<FAST>(-2.0f * fabsf(s));
+  const float rE = f_div<FAST>(1.0f, 1.0f + E);
+  float h;
+  if constexpr (FAST)
+    h = copysignf((1.0f - E) * rE, s);
+  else
+    h = tanhf(s);
+  const float hp = 4.0f * E * rE * rE;
+  float uh[DPL];
+  float sua = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    uh[i] = fmaf(cn, w[i], u[i]);
+    sua += uh[i] * a[i];
+  }
+  const float ua = gsum<G>(sua);
+  const float q = m - cn * 1e-9f;
+  const float hpd = gl * f_div<FAST>(hp, 1.0f + hp * q);
+  const float Ss = hp * ua - 2.0f * q * h * hpd;
+  float Gv[DPL];
+  float swG = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    Gv[i] = h * a[i] + hpd * w[i];
+    swG += w[i] * Gv[i];
+  }
+  const float wGn = f_div<FAST>(gsum<G>(swG), nw2);
+  const float k1 = (sg - 1.0f) * wGn;
+  const float k2 = 2.0f * cn * wGn;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const int jj = j + G * i;
+    if (jj < d) {
+      p[jj] = Gv[i] + k1 * w[i];
+      p[d + jj] = z[i] * Ss + hpd * uh[i] + cn * Gv[i] - k2 * w[i] + k1 * u[i];
+      a[i] = fmaf(w[i], Ss, a[i]);
+    }
+  }
+  if (j == 0) p[2 * d] = Ss;  // the group's lanes read p[2d] above, in lockstep
+}
+
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d, int j,
+                                              float gl) {
+  const float xa = 0.3f * p[0] - 2.0f;
+  const float xb = 0.1f * p[1] + kLogExpm1One;
+  float al, sga, spb, sgb;
+  if constexpr (FAST) {
+    sp_sig1(xa, al, sga);
+    sp_sig1(xb, spb, sgb);
+  } else {
+    al = softplus_tf<false>(xa);
+    sga = f_sigmoid<false>(xa);
+    spb = softplus_tf<false>(xb);
+    sgb = f_sigmoid<false>(xb);
+  }
+  const float be = spb - 1.0f;
+  float dz[DPL];
+  float sr = 0.0f, sda = 0.0f;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    dz[i] = j + G * i < d ? z[i] - p[2 + j + G * i] : 0.0f;
+    sr += fabsf(dz[i]);
+    sda += dz[i] * a[i];
+  }
+  const float r = gsum<G>(sr);
+  const float da = gsum<G>(sda);
+  const float h = f_div<FAST>(1.0f, al + r);
+  const float hh = h * h;
+  const float ab = al * be;
+  const float A = 1.0f + ab * h;
+  const float rB = f_div<FAST>(1.0f, 1.0f + ab * al * hh);
+  const float rA = d > 1 ? f_div<FAST>((float)(d - 1), A) : 0.0f;  // (d-1) / A
+  const float H = ab * da + gl * (ab * rA + 2.0f * ab * al * h * rB);
+  const float g_ab = h * da + gl * (h * rA + al * hh * rB);
+  const float g_al = be * g_ab + gl * ab * hh * rB - hh * H;
+  const float hH = hh * H;
+  const float abh = ab * h;
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const int jj = j + G * i;
+    if (jj < d) {
+      const float sgn = sign0(dz[i]);
+      p[2 + jj] = hH * sgn - abh * a[i];
+      a[i] = A * a[i] - hH * sgn;
+    }
+  }
+  if (j == 0) {
+    p[0] = 0.3f * sga * g_al;
+    p[1] = 0.1f * sgb * al * g_ab;
+  }
+}
+
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ void affine_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d, int j,
+                                              float gl) {
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const int jj = j + G * i;
+    if (jj < d) {
+      const float sc = 1.0f + p[d + jj];
+      p[jj] = a[i];
+      p[d + jj] = z[i] * a[i] + gl * f_div<FAST>(1.0f, sc);
+      a[i] *= sc;
+    }
+  }
+}
+
+template <int G, int DPL, bool FAST>
+__device__ __forceinline__ void base_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* row, int d, int j,
+                                            bool trainable, float gl) {
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const int jj = j + G * i;
+    a[i] = 0.0f;
+    if (jj < d) {
+      if (trainable) {
+        const float xs = kLogExpm1One + 0.1f * row[d + jj];
+        float sps, sgs;
+        if constexpr (FAST) {
+          sp_sig1(xs, sps, sgs);
+        } else {
+          sps = softplus_tf<false>(xs);
+          sgs = f_sigmoid<false>(xs);
+        }
+        const float rs = f_div<FAST>(1.0f, 1e-3f + sps);
+        const float zz = (z[i] - row[jj]) * rs;
+        const float gz = gl * zz * rs;
+        a[i] = -gz;
+        row[jj] = gz;
+        row[d + jj] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+      } else {
+        a[i] = -gl * z[i];
+      }
+    }
+  }
+}
+
+}  // namespace nfn

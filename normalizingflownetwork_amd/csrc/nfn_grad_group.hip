@@ -1,0 +1,266 @@
+// nfn_grad_group.hip — the fused backward for wide events (d >= 4; config C3),
+// structured like chain_group_kernel: a persistent grid whose every wave owns a
+// stream of R = 64/G-sample tiles, one G-lane group per sample (lane j holds the
+// DPL dimensions j, j + G, ...), inner products as DPP group sums.
+// Per wave LDS slot: the tile's parameter rows (stride S from group_lds_stride)
+// followed by the lanes' flow inputs zh[(k * DPL + i) * 64 + lane].  The next
+// tile's rows (NV float4 per lane), y and upstream gradients are prefetched into
+// registers (non-temporal) while the current tile runs forward + reverse; the
+// reverse pass overwrites each flow's block with its gradient in LDS and the tile
+// goes back to HBM with the load's (row, 16-byte column) slot map.
+// Compiled twice: -DNFN_FAST=1 and -DNFN_FAST=0.
+#include "nfn_grad_device.h"
+#include "nfn_launch.h"
+
+#ifndef NFN_FAST
+#error "compile with -DNFN_FAST=0 or -DNFN_FAST=1"
+#endif
+
+namespace nfn {
+namespace {
+
+constexpr bool kFast = NFN_FAST != 0;
+
+__device__ __forceinline__ int flow_width(int id, int d) {
+  return id == NFN_FLOW_PLANAR ? 2 * d + 1 : (id == NFN_FLOW_RADIAL ? d + 2 : 2 * d);
+}
+
+template <int G, int DPL, bool FAST, int NV>
+__global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga) {
+  const ChainArgs& a = ga.c;
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int R = 64 / G;
+  const int sl = lane / G;
+  const int j = lane - sl * G;
+  const int d = a.d;
+  const int K = a.prog.K;
+  const int Q = a.P >> 2;
+  const int S = a.lds_stride;
+  const bool lds4 = (S & 3) == 0;
+  const int64_t rs = a.t_rowstride;
+  const int64_t gts = ga.gt_rowstride;
+  const int slot = R * S + K * DPL * 64;
+  float* tl = lds + wid * slot;
+  float* zh = tl + R * S + lane;
+  const int r00 = lane / Q, c00 = lane - (lane / Q) * Q;
+  const int sq = 64 / Q, sc = 64 - (64 / Q) * Q;
+  const int nslots = R * Q;
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  uint32_t tw[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tw[q] = a.prog.types[q];
+  float corr = 0.0f;
+  if (a.y_mean) {
+    for (int i = 0; i < d; ++i) corr += f_log<FAST>(a.y_std[i]);
+  }
+
+  float4 buf[NV];
+  float ybuf[DPL];
+  float gbuf = 1.0f;
+  bool issued_once = false;
+  auto issue = [&](int64_t tile) {
+    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    issued_once = true;
+    const int64_t b0 = tile * R;
+    const int nr = (int)min((int64_t)R, a.B - b0);
+    const float* base = a.t + b0 * rs;
+    int r = r00, c = c00;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      if (lane + k * 64 < nslots && r < nr) buf[k] = load_row4<true>(base + (int64_t)r * rs + 4 * c);
+      r += sq;
+      c += sc;
+      if (c >= Q) {
+        c -= Q;
+        r += 1;
+      }
+    }
+    if (sl < nr) {
+#pragma unroll
+      for (int i = 0; i < DPL; ++i)
+        ybuf[i] = (j + G * i < d) ? a.y[(b0 + sl) * a.y_bstride + j + G * i] : 0.0f;
+      if (ga.g_out) gbuf = ga.g_out[b0 + sl];
+    }
+  };
+
+  int64_t tile = u0;
+  if (tile < a.ntiles) issue(tile);
+  for (; tile < a.ntiles; tile += ustep) {
+    const int64_t b0 = tile * R;
+    const int nr = (int)min((int64_t)R, a.B - b0);
+    {
+      int r = r00, c = c00;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (lane + k * 64 < nslots && r < nr) {
+          float* dst = tl + r * S + 4 * c;
+          if (lds4) {
+            *reinterpret_cast<float4*>(dst) = buf[k];
+          } else {
+            dst[0] = buf[k].x;
+            dst[1] = buf[k].y;
+            dst[2] = buf[k].z;
+            dst[3] = buf[k].w;
+          }
+        }
+        r += sq;
+        c += sc;
+        if (c >= Q) {
+          c -= Q;
+          r += 1;
+        }
+      }
+    }
+    float z[DPL];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      const int jj = j + G * i;
+      z[i] = ybuf[i];
+      if (a.y_mean && jj < d) z[i] = f_div<FAST>(z[i] - a.y_mean[jj], a.y_std[jj]);
+    }
+    const float gl = gbuf;
+    wave_lds_sync();
+    if (tile + ustep < a.ntiles) issue(tile + ustep);
+    if (sl < nr) {
+      float* row = tl + sl * S;
+      // forward, keeping each flow's input
+      float ildj = 0.0f, dimterm = 0.0f;
+      int off = a.P;
+      for (int k = 0; k < K; ++k) {
+        const int id = flow_type_at(tw, k);
+        off -= flow_width(id, d);
+        const float* p = row + off;
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) zh[(k * DPL + i) * 64] = z[i];
+        if (id == NFN_FLOW_PLANAR) {
+          ildj = ildj + planar_gd<G, DPL, FAST>(z, p, d, j);
+        } else if (id == NFN_FLOW_RADIAL) {
+          ildj = ildj + radial_gd<G, DPL, FAST>(z, p, d, j);
+        } else {
+#pragma unroll
+          for (int i = 0; i < DPL; ++i) {
+            if (j + G * i < d) {
+              const float s1 = 1.0f + p[d + j + G * i];
+              z[i] = z[i] * s1 + p[j + G * i];
+              dimterm += f_log<FAST>(fabsf(s1));
+            }
+          }
+        }
+      }
+      if (a.out) {
+        float bt = 0.0f;
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) {
+          const int jj = j + G * i;
+          if (jj < d) {
+            if (a.trainable) {
+              const float s1 = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + jj]);
+              const float zz = f_div<FAST>(z[i] - row[jj], s1);
+              bt += -0.5f * (zz * zz) - f_log<FAST>(s1);
+            } else {
+              bt += -0.5f * (z[i] * z[i]);
+            }
+          }
+        }
+        const float lp = ((gsum<G>(dimterm + bt) - kHalfLog2Pi * (float)d) + ildj) - corr;
+        if (j == 0) __builtin_nontemporal_store(lp, a.out + b0 + sl);
+      }
+      // reverse pass: flow K-1's block follows the base, flow k-1's follows flow k's
+      float adj[DPL];
+      base_gd_bwd<G, DPL, FAST>(z, adj, row, d, j, a.trainable != 0, gl);
+      off = a.trainable ? 2 * d : 0;
+      for (int k = K - 1; k >= 0; --k) {
+        const int id = flow_type_at(tw, k);
+        float zk[DPL];
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) zk[i] = zh[(k * DPL + i) * 64];
+        float* p = row + off;
+        if (id == NFN_FLOW_PLANAR)
+          planar_gd_bwd<G, DPL, FAST>(zk, adj, p, d, j, gl);
+        else if (id == NFN_FLOW_RADIAL)
+          radial_gd_bwd<G, DPL, FAST>(zk, adj, p, d, j, gl);
+        else
+          affine_gd_bwd<G, DPL, FAST>(zk, adj, p, d, j, gl);
+        off += flow_width(id, d);
+      }
+      if (ga.grad_y) {
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) {
+          const int jj = j + G * i;
+          if (jj < d) ga.grad_y[(b0 + sl) * d + jj] = a.y_std ? f_div<FAST>(adj[i], a.y_std[jj]) : adj[i];
+        }
+      }
+    }
+    wave_lds_sync();
+    if (ga.grad_t) {
+      float* gbase = ga.grad_t + b0 * gts;
+      int r = r00, c = c00;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (lane + k * 64 < nslots && r < nr) {
+          const float* src = tl + r * S + 4 * c;
+          f32x4 v;
+          if (lds4) {
+            const float4 t4 = *reinterpret_cast<const float4*>(src);
+            v = f32x4{t4.x, t4.y, t4.z, t4.w};
+          } else {
+            v = f32x4{src[0], src[1], src[2], src[3]};
+          }
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(gbase + (int64_t)r * gts + 4 * c));
+        }
+        r += sq;
+        c += sc;
+        if (c >= Q) {
+          c -= Q;
+          r += 1;
+        }
+      }
+    }
+  }
+}
+
+template <int G, int DPL, int NV>
+void launch_gg(const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = chain_grad_group_kernel<G, DPL, kFast, NV>;
+  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (ga.c.ntiles + 3) / 4);  // 4 wave teams per WG
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, ga);
+}
+
+template <int G, int DPL>
+bool launch_gg_nv(int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* g) {
+  if (nv <= 4)
+    launch_gg<G, DPL, 4>(ga, lds, s, g);
+  else if (nv <= 6)
+    launch_gg<G, DPL, 6>(ga, lds, s, g);
+  else if (nv <= 9)
+    launch_gg<G, DPL, 9>(ga, lds, s, g);
+  else if (nv <= 12)
+    launch_gg<G, DPL, 12>(ga, lds, s, g);
+  else if (nv <= 16)
+    launch_gg<G, DPL, 16>(ga, lds, s, g);
+  else
+    return false;
+  return true;
+}
+
+}  // namespace
+
+#if NFN_FAST
+bool launch_grad_group_fast(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid) {
+#else
+bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s,
+                               int64_t* grid) {
+#endif
+  if (G == 4 && DPL == 1) return launch_gg_nv<4, 1>(nv, ga, lds, s, grid);
+  if (G == 4 && DPL == 2) return launch_gg_nv<4, 2>(nv, ga, lds, s, grid);
+  if (G == 4 && DPL == 4) return launch_gg_nv<4, 4>(nv, ga, lds, s, grid);
+  if (G == 8 && DPL == 4) return launch_gg_nv<8, 4>(nv, ga, lds, s, grid);
+  return false;
+}
+
+}  // namespace nfn

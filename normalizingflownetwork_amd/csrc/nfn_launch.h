@@ -55,6 +55,13 @@ void launch_flow(bool fast, int dm, int32_t flow_id, const float* z, int64_t z_b
                  int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, hipStream_t s);
 // nfn_grad.hip
 void launch_grad(bool fast, int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_t s);
+// wave-owned persistent form; false if (dm, nv) has no instance
+bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_block, int waves_per_block,
+                      hipStream_t s, int64_t* grid);
+// nfn_grad_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance
+bool launch_grad_group_fast(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid);
+bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s,
+                               int64_t* grid);
 // nfn_misc.hip
 void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);

@@ -66,6 +66,7 @@ for s in $STEPS; do
     mode) run mode 300 python tools/microbench.py mode ;;
     valu) run valu 300 python tools/microbench.py valu ;;
     c3micro) run c3micro 300 python tools/microbench.py c3 ;;
+    gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
     pf2) run pf2 300 python tools/microbench.py pf2 ;;
     *) echo "unknown step $s" ;;
   esac

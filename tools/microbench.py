@@ -73,8 +73,61 @@ def run(cfg, variants, reps=20, rounds=3):
     return res
 
 
+def run_grad(cfg, variants, reps=10, rounds=3):
+    """Fused backward variants (GradLauncher), same interleaving."""
+    ft, d, B, S = CFG[cfg]
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    t = torch.randn((B, P), generator=gen, device="cuda")
+    g = torch.full((B,), -1.0 / B, device="cuda")
+    L = ops.GradLauncher(y, t, ft, d, True, g_out=g)
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    times = {v["name"]: [] for v in variants}
+    outs = {}
+    for r in range(rounds):
+        for v in variants:
+            for k, val in v.get("env", {}).items():
+                os.environ[k] = str(val)
+            ops.set_math_mode(v.get("math", "fast"))
+            for _ in range(2):
+                L.launch(sh)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in evs:
+                e0.record(stream)
+                L.launch(sh)
+                e1.record(stream)
+            torch.cuda.synchronize()
+            times[v["name"]].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+            if r == 0:
+                outs[v["name"]] = L.grad_t.clone()
+            for k in v.get("env", {}):
+                os.environ.pop(k, None)
+    ref = outs[variants[0]["name"]]
+    bpl = B * (8 * d + 8 * P + 4)
+    for v in variants:
+        ms = float(np.median(times[v["name"]]))
+        diff = float((outs[v["name"]] - ref).abs().max().item())
+        print(json.dumps({"cfg": cfg, "mode": "grad", "variant": v["name"], "ms": ms, "GBps": bpl / ms / 1e6,
+                          "frac8TBs": bpl / ms / 1e6 / 8000, "maxdiff_vs_first": diff,
+                          "rounds_ms": times[v["name"]]}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "grad":
+        v = [{"name": "wave", "env": {}},
+             {"name": "tile_v1", "env": {"NFN_GRAD_WAVE": 0}},
+             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "v1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_GRAD_WAVE": 0}},
+             {"name": "v1_compute_only", "env": {"NFN_ABLATE_LOADS": 1, "NFN_GRAD_WAVE": 0}}]
+        run_grad("C2", v)
+        run_grad("C3", [{"name": "group", "env": {}}, {"name": "tile_v1", "env": {"NFN_GRAD_GROUP": 0}},
+                        {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                        {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}])
+        return
     if which[0] == "c3":  # wide-event group kernel
         v = [{"name": "auto_g4x2", "env": {}},
              {"name": "g8x1", "env": {"NFN_GROUP_LANES": 8}},
