@@ -60,6 +60,16 @@ for s in $STEPS; do
     prof_grad)
       { cd /tmp; run rocprof_grad 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_grad" -o grad -- \
         python3 "$ROOT/bench.py" --mode grad --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_c3)
+      { cd /tmp; run pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_c3" -o f -- \
+        python3 "$ROOT/bench.py" --config C3 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_c3" -o w -- \
+        python3 "$ROOT/bench.py" --config C3 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_grad)
+      { cd /tmp; run pmc_fetch_grad 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_grad" -o f -- \
+        python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write_grad 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_grad" -o w -- \
+        python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
     debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
     mem) run mem 300 python tools/microbench.py mem ;;
