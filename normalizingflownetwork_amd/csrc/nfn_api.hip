@@ -72,7 +72,8 @@ int dm_for(int d) {
 }
 
 struct TileGeom {
-  int rows;
+  int rows;     // samples per tile
+  int threads;  // workgroup size (>= 64: one full wave even for narrow tiles)
   int lds_stride;
   size_t lds_bytes;
 };
@@ -87,7 +88,11 @@ TileGeom tile_geom(int P) {
     if (r >= 64 && r <= kMaxBlock && r % 64 == 0) rows = r;
   }
   while (rows > 64 && (size_t)rows * row_bytes > (size_t)kLdsTileBudget) rows -= 64;
+  // very wide rows (up to NFN_MAX_FLOWS x (2 NFN_MAX_DIMS + 1) floats): fewer samples
+  // per tile so the tile fits the 160 KiB of LDS a workgroup may hold
+  while (rows > 1 && (size_t)rows * row_bytes > (size_t)kLdsMaxBytes) rows >>= 1;
   g.rows = rows;
+  g.threads = std::max(rows, 64);
   g.lds_bytes = P > 0 ? (size_t)rows * row_bytes : 0;
   return g;
 }
@@ -128,7 +133,10 @@ void group_shape(int dm, int want_g, int* G, int* DPL) {
 }
 
 // One fp64 partial per workgroup at the smallest tile (64 rows).
-int64_t partials_capacity(int64_t B) { return (B + 63) / 64; }
+int64_t partials_capacity(int64_t B, int P) {
+  const int rows = std::min(64, tile_geom(P < 0 ? 0 : P).rows);
+  return (B + rows - 1) / rows;
+}
 
 // Draw ranges per tile for the posterior: enough (tile, range) units for every
 // resident team (~2 per team: 8 workgroups of 256 rows, or 32 waves of 64 rows,
@@ -240,7 +248,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
       a.nsplit = nsplit;
       a.dps = (S + nsplit - 1) / nsplit;
       a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges
-      a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B));
+      a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B, P));
       if (fast) launch_persistent_fast(true, dm, Q, a, g.rows, lds_p, s, &nblk);
       else launch_persistent_precise(true, dm, Q, a, g.rows, lds_p, s, &nblk);
       if (a.nsplit > 1) {
@@ -254,7 +262,10 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
       else launch_persistent_precise(false, dm, Q, a, g.rows, lds_p, s, &nblk);
     }
   } else {
-    const dim3 grid((unsigned)nblk), block((unsigned)g.rows);
+    if ((size_t)g.rows * ((size_t)g.lds_stride * sizeof(float)) > (size_t)kLdsMaxBytes)
+      return fail(NFN_E_SHAPE, "parameter row too wide for LDS");
+    a.tile_rows = g.rows;
+    const dim3 grid((unsigned)nblk), block((unsigned)g.threads);
     launch_tile(use_fast_math(), posterior, dm, a, grid, block, g.lds_bytes, s);
   }
   int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
@@ -391,13 +402,13 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   (void)d;
   (void)P;
   if (B <= 0) return 0;
-  return 1 + partials_capacity(B);  // [count | partials]
+  return 1 + partials_capacity(B, P);  // [count | partials]
 }
 
 int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   if (B <= 0) return 0;
   // [count | partials | draw-split region: (max, sum) float2 per (range, sample)]
-  return 1 + partials_capacity(B) + (int64_t)posterior_split(B, tile_geom(P < 0 ? 0 : P).rows) * B;
+  return 1 + partials_capacity(B, P) + (int64_t)posterior_split(B, tile_geom(P < 0 ? 0 : P).rows) * B;
 }
 
 int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream) {

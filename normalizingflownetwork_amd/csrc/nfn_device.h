@@ -43,6 +43,7 @@ namespace nfn {
 
 constexpr int kMaxBlock = 256;
 constexpr int kLdsTileBudget = 48 * 1024;  // bytes of LDS per workgroup for the tile
+constexpr int kLdsMaxBytes = 156 * 1024;   // dynamic LDS a tile workgroup may take (160 KiB - static)
 constexpr float kSoftplusThr = 13.942384719848633f;  // -(log(FLT_EPSILON) + 2), TF SoftplusOp
 constexpr float kLogExpm1One = 0.54132485461291810f; // log(expm1(1))
 constexpr float kHalfLog2Pi = 0.91893853320467274f;   // 0.5*log(2*pi)
@@ -93,6 +94,7 @@ struct ChainArgs {
   int32_t nsplit;      // posterior: draw ranges per tile (1 = no split)
   int32_t dps;         // posterior: draws per range
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
+  int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   FlowProgram prog;
 };
 
@@ -566,7 +568,7 @@ template <int DM, bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
-  const int rows = blockDim.x;
+  const int rows = a.tile_rows > 0 ? a.tile_rows : blockDim.x;
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * rows;
   const int nr = (int)min((int64_t)rows, a.B - b0);
@@ -598,7 +600,7 @@ template <int DM, bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
-  const int rows = blockDim.x;
+  const int rows = a.tile_rows > 0 ? a.tile_rows : blockDim.x;
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * rows;
   const int nr = (int)min((int64_t)rows, a.B - b0);

@@ -330,3 +330,36 @@ def test_load_modes_bitwise_equal(mode, gpu):
     assert torch.equal(got, ref)
     assert float(s.item()) == pytest.approx(float(got.double().sum().item()), rel=1e-12)
     np.testing.assert_allclose(pgot.cpu().numpy(), pref.cpu().numpy(), rtol=2e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize("d,K", [(32, 64), (1, 64), (16, 40), (5, 64)])
+def test_maximum_sizes(d, K, math_mode):
+    """NFN_MAX_DIMS / NFN_MAX_FLOWS (include/nfn.h): the widest parameter rows
+    (d=32, 64 flows: P = 4224 floats) run on narrow tiles; forward, posterior and
+    backward against the oracle on a ragged batch."""
+    from normalizingflownetwork_amd import ops
+    from oracle import nfn_grad_oracle as G
+
+    rng = np.random.default_rng(d * 100 + K)
+    ft = tuple(rng.choice(["planar", "radial", "affine"], size=K))
+    P = O.total_param_size(ft, d, True)
+    B = 37
+    y = rng.standard_normal((B, d)).astype(np.float32)
+    t = (0.3 * rng.standard_normal((B, P))).astype(np.float32)
+    lp, s = ops.chain_log_prob(torch.from_numpy(y).cuda(), torch.from_numpy(t).cuda(), ft, d, True,
+                               want_sum=True)
+    ref64 = O.chain_log_prob(y, t, ft, d, True, np.float64)
+    ref32 = O.chain_log_prob(y, t, ft, d, True, np.float32)
+    assert_within(lp.cpu().numpy(), ref64, ref32, f"max d={d} K={K}")
+    assert abs(s.item() - ref64.sum()) <= 1e-4 * max(1.0, abs(ref64.sum()))
+    td = torch.from_numpy(np.stack([t, t[::-1].copy()])).cuda()
+    post, _ = ops.posterior_lse(torch.from_numpy(y).cuda(), td, ft, d, True)
+    r64 = O.posterior_lse(y, np.stack([t, t[::-1]]), ft, d, True, dtype=np.float64)
+    r32 = O.posterior_lse(y, np.stack([t, t[::-1]]), ft, d, True, dtype=np.float32)
+    assert_within(post.cpu().numpy(), r64, r32, f"max posterior d={d} K={K}")
+    _, gt, gy = ops.chain_log_prob_grad(torch.from_numpy(y).cuda(), torch.from_numpy(t).cuda(), ft, d, True)
+    gt64, gy64, dev_t, dev_y = G.fp32_spread(y, t, ft, d, True, n_perturbed=1)
+    for got, ref, dev in ((gt.cpu().numpy(), gt64, dev_t), (gy.cpu().numpy(), gy64, dev_y)):
+        ok = np.isfinite(ref)
+        ratio = np.abs(got - ref)[ok] / G.grad_tolerance(ref, dev)[ok]
+        assert ratio.size == 0 or ratio.max() <= 1.0, f"grad d={d} K={K}: max err/bound {ratio.max():.3g}"
