@@ -37,6 +37,9 @@
  *                             reference trains: model.compile(loss=NLL) / fit
  *                                                    estimators/BaseEstimator.py:19-31, 55-59,
  *                                                    estimators/MaximumLikelihoodNNEstimator.py:33-35
+ *   nfn_chain_logprob_grid_f32
+ *                          <- the per-grid-point loop of dist.prob(y[i]) over a batch of x in
+ *                             evaluation/visualization/flow_plotting.py:33-53 (plot_model)
  *   nfn_flow_fwd_ldj_f32   <- PlanarFlow._forward/_forward_log_det_jacobian
  *                                                    estimators/normalizing_flows/PlanarFlow.py:20-80
  *                             RadialFlow._forward/_forward_log_det_jacobian
@@ -138,6 +141,17 @@ int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const floa
                                    int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
                                    const float* y_mean, const float* y_std, const float* g_out, float* out_logp,
                                    float* grad_t, int64_t grad_t_rowstride, float* grad_y, void* stream);
+
+/*
+ * Density on a grid of y values shared by every parameter row:
+ *   out[g * out_gstride + b] = logp(y_grid[g] | t_b) [- sum log y_std]
+ *   y_grid : (G, d) rows at y_gstride floats (0 = one row);  t : as nfn_chain_logprob_f32
+ *   out    : (G, B) with out_gstride >= B
+ */
+int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32_t G, const float* t,
+                                   int64_t t_rowstride, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
+                                   int32_t trainable_base, const float* y_mean, const float* y_std, float* out,
+                                   int64_t out_gstride, void* stream);
 
 /*
  * One bijector, forward direction: z_out = f(z), ldj_out = log|det df/dz| (B,).

@@ -48,6 +48,11 @@ SIGNATURES = {
         [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp, _vp, _vp,
          _c_int64, _vp, _vp],
     ),
+    "nfn_chain_logprob_grid_f32": (
+        _c_int32,
+        [_vp, _c_int64, _c_int32, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp,
+         _c_int64, _vp],
+    ),
     "nfn_comm_unique_id": (_c_int32, [_vp]),
     "nfn_comm_init": (_c_int32, [ctypes.POINTER(_vp), _c_int32, _vp, _c_int32]),
     "nfn_comm_destroy": (_c_int32, [_vp]),

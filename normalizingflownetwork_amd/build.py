@@ -33,6 +33,7 @@ UNITS = [
     ("grad", "nfn_grad.hip", []),
     ("grad_group_fast", "nfn_grad_group.hip", ["-DNFN_FAST=1"]),
     ("grad_group_precise", "nfn_grad_group.hip", ["-DNFN_FAST=0"]),
+    ("grid", "nfn_grid.hip", []),
     ("comm", "nfn_comm.hip", []),
 ]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")

@@ -362,6 +362,56 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   return check_hip("chain_grad_kernel launch");
 }
 
+int32_t run_grid(const float* y_grid, int64_t y_gstride, int32_t G, const float* t, int64_t t_rowstride, int64_t B,
+                 int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                 const float* y_std, float* out, int64_t out_gstride, void* stream) {
+  g_last_error.clear();
+  GridArgs ga;
+  memset(&ga, 0, sizeof(ga));
+  ChainArgs& a = ga.c;
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  if (B < 0 || G < 0) return fail(NFN_E_SHAPE, "batch and grid sizes must be >= 0");
+  if (y_gstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
+  if (y_gstride != 0 && y_gstride < d) return fail(NFN_E_SHAPE, "y_grid stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
+  if (out_gstride < B) return fail(NFN_E_SHAPE, "out grid stride < batch size");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  if (B == 0 || G == 0) return NFN_OK;
+  if (!y_grid || !out) return fail(NFN_E_NULLPTR, "y_grid or out is NULL");
+  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
+  const TileGeom g = tile_geom(P);
+  if ((size_t)g.rows * ((size_t)g.lds_stride * sizeof(float)) > (size_t)kLdsMaxBytes)
+    return fail(NFN_E_SHAPE, "parameter row too wide for LDS");
+  a.t = t;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.t_rowstride = t_rowstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = g.lds_stride;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = 1;
+  a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  a.tile_rows = g.rows;
+  ga.y_grid = y_grid;
+  ga.y_gstride = y_gstride;
+  ga.out = out;
+  ga.out_gstride = out_gstride;
+  ga.G = G;
+  const int64_t ntiles = (B + g.rows - 1) / g.rows;
+  if (ntiles > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  // enough (tile, grid-chunk) workgroups to fill the chip: ~4 per CU
+  const int64_t want = std::max<int64_t>(1, ((int64_t)cu_count() * 4 + ntiles - 1) / ntiles);
+  int64_t nchunks = std::min<int64_t>({(int64_t)G, want, 65535});
+  ga.gchunk = (int32_t)((G + nchunks - 1) / nchunks);
+  nchunks = (G + ga.gchunk - 1) / ga.gchunk;
+  launch_grid(use_fast_math(), dm_for(d), ga, dim3((unsigned)ntiles, (unsigned)nchunks), dim3((unsigned)g.threads),
+              g.lds_bytes, reinterpret_cast<hipStream_t>(stream));
+  return check_hip("chain_grid_kernel launch");
+}
+
 }  // namespace
 }  // namespace nfn
 
@@ -440,6 +490,14 @@ int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const floa
                                    float* grad_t, int64_t grad_t_rowstride, float* grad_y, void* stream) {
   return run_grad(y, y_bstride, t, t_rowstride, B, d, flow_ids, K, trainable_base, y_mean, y_std, g_out, out_logp,
                   grad_t, grad_t_rowstride, grad_y, stream);
+}
+
+int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32_t G, const float* t,
+                                   int64_t t_rowstride, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
+                                   int32_t trainable_base, const float* y_mean, const float* y_std, float* out,
+                                   int64_t out_gstride, void* stream) {
+  return run_grid(y_grid, y_gstride, G, t, t_rowstride, B, d, flow_ids, K, trainable_base, y_mean, y_std, out,
+                  out_gstride, stream);
 }
 
 int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,

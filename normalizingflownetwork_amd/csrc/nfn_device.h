@@ -98,6 +98,17 @@ struct ChainArgs {
   FlowProgram prog;
 };
 
+// Density grid (nfn_grid.hip): y values shared by all parameter rows.
+struct GridArgs {
+  ChainArgs c;
+  const float* y_grid;   // (G, d) rows at y_gstride floats
+  int64_t y_gstride;
+  float* out;            // (G, B): out[g * out_gstride + b]
+  int64_t out_gstride;
+  int32_t G;
+  int32_t gchunk;        // grid points per workgroup (blockIdx.y walks the chunks)
+};
+
 // Backward (nfn_grad.hip): the forward's arguments plus the gradient outputs.
 struct GradArgs {
   ChainArgs c;

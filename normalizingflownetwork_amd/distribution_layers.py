@@ -166,6 +166,19 @@ class FlowDistribution:
     def prob(self, y, y_mean=None, y_std=None):
         return torch.exp(self.log_prob(y, y_mean, y_std))
 
+    def log_prob_grid(self, y_grid, y_mean=None, y_std=None) -> torch.Tensor:
+        """``log_prob`` of each grid value (G, d) under every batch member: (G, *batch_shape)."""
+        P = _shape(self._t)[-1]
+        t = ops.as_device_f32(self._t)
+        bshape = tuple(t.shape[:-1])
+        t2 = t.reshape(-1, P) if t.dim() != 2 else t
+        yg = ops.as_device_f32(y_grid).reshape(-1, self._n_dims)
+        out = ops.chain_log_prob_grid(yg, t2, self._flow_types, self._n_dims, self._trainable, y_mean, y_std)
+        return out.reshape((yg.shape[0],) + bshape)
+
+    def prob_grid(self, y_grid, y_mean=None, y_std=None) -> torch.Tensor:
+        return torch.exp(self.log_prob_grid(y_grid, y_mean, y_std))
+
     def sample(self, *args, **kwargs):
         raise NotImplementedError(
             "the inverted flows cannot sample (reference DistributionLayers.py:223-226, 240)"

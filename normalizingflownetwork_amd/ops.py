@@ -219,6 +219,41 @@ def log_prob(y, t, flow_types: Sequence[str], n_dims: int, trainable_base: bool,
     return _ChainLogProb.apply(y, t, tuple(flow_types), int(n_dims), bool(trainable_base), y_mean, y_std)
 
 
+def chain_log_prob_grid(
+    y_grid,
+    t,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+) -> torch.Tensor:
+    """``log_prob`` of every grid value ``y_grid[g]`` (G, d) under every parameter row
+    ``t[b]`` (B, P): returns (G, B) — the density-grid evaluation of
+    ``flow_plotting.plot_model`` (``evaluation/visualization/flow_plotting.py:33-53``) in
+    one kernel."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    yg = _prep_2d(y_grid, n_dims, "y_grid", dev)
+    t = _prep_2d(t, P, "t", dev) if P > 0 else torch.zeros((1, 1), dtype=torch.float32, device=dev)
+    G = int(yg.shape[0])
+    B = int(t.shape[0]) if P > 0 else 1
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+        assert ym.numel() == n_dims and ys.numel() == n_dims
+    out = torch.empty((G, B), dtype=torch.float32, device=dev)
+    ids, k = flow_ids(flow_types)
+    rc = _lib.load().nfn_chain_logprob_grid_f32(
+        _ptr(yg), int(yg.stride(0)) if G > 1 else 0, G, _ptr(t), _row_stride(t) if P > 0 else 0, B, int(n_dims),
+        ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys), _ptr(out), B,
+        _stream(),
+    )
+    _lib.check(rc, "nfn_chain_logprob_grid_f32")
+    return out
+
+
 def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, want_ldj: bool = True):
     """One bijector: ``(forward(z), forward_log_det_jacobian(z))`` (either may be None)."""
     dev = _device()

@@ -127,3 +127,15 @@ def test_comm_entry_points_validate_before_rccl(native_lib):
     assert native_lib.nfn_allreduce_mean(None, None, 1, None, None, None) == _lib.NFN_E_NULLPTR
     assert "allreduce" in _lib.last_error()
     assert native_lib.nfn_comm_destroy(None) == _lib.NFN_OK
+
+
+def test_grid_entry_point_validates(native_lib):
+    from normalizingflownetwork_amd import _lib
+
+    ids = _ids("planar", "radial")
+    p_ids = ctypes.cast(ids, ctypes.c_void_p)
+    f = native_lib.nfn_chain_logprob_grid_f32
+    assert f(None, 1, 4, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 10, None) == _lib.NFN_E_NULLPTR
+    assert f(None, 1, -1, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 10, None) == _lib.NFN_E_SHAPE
+    assert f(None, 1, 4, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 9, None) == _lib.NFN_E_SHAPE
+    assert f(None, 1, 0, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 10, None) == _lib.NFN_OK

@@ -1,0 +1,76 @@
+"""Density-grid evaluation (flow_plotting.py:33-53) against
+the oracle: every (grid value, parameter row) pair, with and without the fused y
+normalisation, broadcast parameter rows and ragged sizes; and the heatmap helper
+against a per-row loop of ``dist.prob``."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nfn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["fast", "precise"])
+def math_mode(request, gpu):
+    from normalizingflownetwork_amd import ops
+
+    prev = ops.set_math_mode(request.param)
+    yield request.param
+    ops.set_math_mode(prev)
+
+
+def _ref(yg, t, ft, d, tr, ym=None, ys=None):
+    r64 = np.stack([O.log_pdf(np.broadcast_to(g, (1, d)), t, ft, d, tr, ym, ys, np.float64) for g in yg])
+    r32 = np.stack([O.log_pdf(np.broadcast_to(g, (1, d)), t, ft, d, tr, ym, ys, np.float32) for g in yg])
+    return r64, r32
+
+
+@pytest.mark.parametrize("ft,d,B,G", [(("planar", "radial") * 5, 1, 300, 17), (("radial",) * 3, 1, 1, 101),
+                                      (("affine", "planar", "radial"), 3, 129, 9),
+                                      (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 70, 33)])
+def test_grid_matches_oracle(math_mode, ft, d, B, G):
+    from normalizingflownetwork_amd import ops
+
+    rng = np.random.default_rng(B + G)
+    P = O.total_param_size(ft, d, True)
+    t = rng.standard_normal((B, P)).astype(np.float32)
+    yg = rng.standard_normal((G, d)).astype(np.float32) * 2
+    out = ops.chain_log_prob_grid(torch.from_numpy(yg).cuda(), torch.from_numpy(t).cuda(), ft, d, True)
+    r64, r32 = _ref(yg, t, ft, d, True)
+    assert out.shape == (G, B)
+    bound = O.tolerance_bound(r64, r32)
+    assert np.all(np.abs(out.cpu().numpy() - r64) <= bound)
+    ym, ys = np.linspace(-0.2, 0.3, d).astype(np.float32), np.linspace(0.5, 2.0, d).astype(np.float32)
+    outn = ops.chain_log_prob_grid(torch.from_numpy(yg).cuda(), torch.from_numpy(t).cuda(), ft, d, True, ym, ys)
+    r64, r32 = _ref(yg, t, ft, d, True, ym, ys)
+    assert np.all(np.abs(outn.cpu().numpy() - r64) <= O.tolerance_bound(r64, r32))
+    # a broadcast parameter row gives the same column for every b
+    out1 = ops.chain_log_prob_grid(torch.from_numpy(yg).cuda(), torch.from_numpy(t[:1]).cuda(), ft, d, True)
+    assert torch.equal(out1[:, 0], out[:, 0])
+
+
+def test_grid_equals_per_row_prob(gpu):
+    """flow_plotting.plot_model's loop (dist.prob(y[i]) per grid row) == the grid kernel."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+    from normalizingflownetwork_amd.flow_plotting import model_density_heatmap
+
+    class _Model:  # the surface plot_model uses: __call__(x) -> dist, y_mean, y_std
+        def __init__(self):
+            self.layer = InverseNormalizingFlowLayer(("radial", "planar"), 1, True)
+            rng = np.random.default_rng(3)
+            self.W = rng.standard_normal((1, self.layer.get_total_param_size())).astype(np.float32)
+            self.y_mean = np.array([0.4], np.float32)
+            self.y_std = np.array([1.7], np.float32)
+
+        def __call__(self, x):
+            return self.layer(torch.from_numpy(np.asarray(x, np.float32) @ self.W).cuda())
+
+    m = _Model()
+    x = np.linspace(-2, 2, 50, dtype=np.float32).reshape(-1, 1)
+    heat = model_density_heatmap(x, m, (-3, 3), y_num=40)
+    dist = m(x)
+    y = (np.linspace(3, -3, 40).reshape(40, 1) - m.y_mean) / m.y_std
+    loop = np.stack([dist.prob(y[i].astype(np.float32)).cpu().numpy() for i in range(40)]) / np.sum(m.y_std)
+    np.testing.assert_allclose(heat, loop, rtol=1e-5, atol=1e-30)  # exp of log_prob < -87 is denormal
