@@ -95,6 +95,35 @@ def cpu_baseline_grad(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 1
     }
 
 
+def cpu_baseline_dense(cfg: str, H: int, seconds: float = 12.0, sample_rows: int = 1 << 20) -> dict:
+    """Reference-path stand-in for --mode dense: numpy fp32 t = h W + b (one BLAS GEMM,
+    as Keras' Dense) followed by the op-by-op chain restatement, 1 thread."""
+    from oracle import nfn_oracle as O
+
+    ft, d, _, _ = CONFIGS[cfg]
+    P = O.total_param_size(ft, d, True)
+    rng = np.random.default_rng(22)
+    y = rng.standard_normal((sample_rows, d)).astype(np.float32)
+    h = rng.standard_normal((sample_rows, H)).astype(np.float32)
+    W = (rng.standard_normal((H, P)) / np.sqrt(H)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(P)).astype(np.float32)
+    run = lambda: O.chain_log_prob(y, h @ W + b, ft, d, True, np.float32)  # noqa: E731
+    from threadpoolctl import threadpool_limits
+
+    with threadpool_limits(limits=1):  # one BLAS thread: the baseline is single-core
+        run()
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run()
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+    return {"value": reps * sample_rows / el, "unit": "evals/s", "cores": 1, "kind": "port",
+            "sample": f"{sample_rows} samples of {cfg} with H={H}: numpy fp32 GEMM + op-by-op chain "
+                      f"(oracle/nfn_oracle.py), {reps} reps in {el:.1f}s"}
+
+
 def cpu_baseline(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 20) -> dict:
     """The reference-path stand-in timed on this host: the oracle's fp32 op-by-op
     numpy restatement (whole-batch ops, TF-eager op order) on a bounded slice."""
@@ -157,9 +186,11 @@ def main():
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
-    ap.add_argument("--mode", default="forward", choices=["forward", "grad"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense"],
                     help="forward = fused log_prob (the headline); grad = the fused backward of the "
-                         "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient)")
+                         "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient); dense = the "
+                         "output Dense layer (H -> P) fused into the chain, streaming h instead of t")
+    ap.add_argument("--hidden", type=int, default=16, help="--mode dense: hidden width H")
     ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
                     help="N > 1 mean all-reduce: torch.distributed, or the library's own RCCL "
                          "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
@@ -181,7 +212,17 @@ def main():
     y = torch.randn((B, d), generator=gen, device=dev)
     t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
     grad_mode = args.mode == "grad"
-    if grad_mode:
+    dense_mode = args.mode == "dense"
+    if dense_mode:
+        assert S is None, "--mode dense covers the plain chain configs"
+        H = args.hidden
+        del t
+        hgen = torch.Generator(device=dev).manual_seed(122 + rank)
+        h = torch.randn((B, H), generator=hgen, device=dev)
+        Wd = torch.randn((H, P), generator=hgen, device=dev) / float(np.sqrt(H))
+        bd = 0.1 * torch.randn((P,), generator=hgen, device=dev)
+        launcher = ops.DenseLauncher(y, h, Wd, bd, ft, d, True)
+    elif grad_mode:
         assert S is None, "--mode grad covers the plain chain configs (C2, C3)"
         g_up = torch.full((B,), -1.0 / B, dtype=torch.float32, device=dev)  # d(mean NLL)/d log_prob
         launcher = ops.GradLauncher(y, t, ft, d, True, g_out=g_up)
@@ -242,6 +283,24 @@ def main():
         kt = torch.tensor([kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
+    unfused_ms = None
+    if dense_mode and rank == 0:
+        # the same x->density work unfused: t = h W + b by the library GEMM (t written to
+        # HBM), then the chain kernel over t (read back) — what the fusion replaces
+        t_buf = torch.empty((B, P), dtype=torch.float32, device=dev)
+        plain = ops.ChainLauncher(y, t_buf, ft, d, True, write_values=True)
+        for _ in range(3):
+            torch.addmm(bd, h, Wd, out=t_buf)
+            plain.launch(sh)
+        pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for e0, e1 in pairs:
+            e0.record(stream)
+            torch.addmm(bd, h, Wd, out=t_buf)
+            plain.launch(sh)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        unfused_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in pairs]))
+        del t_buf, plain
     if grad_mode:
         mean_ll = None
     elif native is not None:
@@ -252,20 +311,33 @@ def main():
     if rank == 0:
         total_evals = evals_per_step * world * args.steps
         value = total_evals / elapsed
-        bytes_launch = algorithmic_bytes_grad(d, P, B) if grad_mode else algorithmic_bytes_per_launch(d, P, B, S)
+        if grad_mode:
+            bytes_launch = algorithmic_bytes_grad(d, P, B)
+        elif dense_mode:
+            bytes_launch = float(B) * (4 * args.hidden + 4 * d + 4) + 4.0 * args.hidden * P + 4.0 * P
+        else:
+            bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.config + ("_grad" if grad_mode else ""), B)
+        traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense"}.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = (cpu_baseline_grad if grad_mode else cpu_baseline)(args.config, seconds=args.cpu_seconds)
+            if grad_mode:
+                cpu = cpu_baseline_grad(args.config, seconds=args.cpu_seconds)
+            elif dense_mode:
+                cpu = cpu_baseline_dense(args.config, args.hidden, seconds=args.cpu_seconds)
+            else:
+                cpu = cpu_baseline(args.config, seconds=args.cpu_seconds)
         wl = {
             "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
             "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
             "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
         }[args.config]
         if grad_mode:
-            kernel_name = "chain_grad_kernel"
+            kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group_kernel"
             metric = f"log_prob backward evals/sec (whole node), {args.config}"
+        elif dense_mode:
+            kernel_name = "chain_dense_kernel"
+            metric = f"Dense(H={args.hidden})->log_prob evals/sec (whole node), {args.config}"
         else:
             kernel_name = {"C2": "chain_persistent_kernel", "C3": "chain_group_kernel",
                            "C5": "chain_persistent_kernel + posterior_merge_kernel"}[args.config]
@@ -312,6 +384,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "mean_log_prob": mean_ll,
+            "unfused_gemm_plus_chain_ms": unfused_ms,
         }
         print(json.dumps(line), flush=True)
     if native is not None:

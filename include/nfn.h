@@ -37,6 +37,11 @@
  *                             reference trains: model.compile(loss=NLL) / fit
  *                                                    estimators/BaseEstimator.py:19-31, 55-59,
  *                                                    estimators/MaximumLikelihoodNNEstimator.py:33-35
+ *   nfn_chain_logprob_dense_f32
+ *                          <- the estimator's output Dense layer (linear) followed by that
+ *                             log_prob: MaximumLikelihoodNNEstimator.py:37-44 (Dense(P)) +
+ *                             DistributionLayers.py:245-255, i.e. model(x).log_prob(y) given the
+ *                             last hidden activations
  *   nfn_chain_logprob_grid_f32
  *                          <- the per-grid-point loop of dist.prob(y[i]) over a batch of x in
  *                             evaluation/visualization/flow_plotting.py:33-53 (plot_model)
@@ -141,6 +146,21 @@ int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const floa
                                    int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
                                    const float* y_mean, const float* y_std, const float* g_out, float* out_logp,
                                    float* grad_t, int64_t grad_t_rowstride, float* grad_y, void* stream);
+
+/*
+ * Output Dense layer fused into the chain: t_b = h_b W + bias (never written to
+ * memory), then exactly nfn_chain_logprob_f32 on t.
+ *   h    : (B, H) rows at h_rowstride floats (>= H, multiple of 4), 16-byte aligned;
+ *          H in {4, 8, 16, 32, 64}
+ *   W    : (H, P) row-major, P = nfn_total_param_size <= 64;  bias : (P,) or NULL
+ *   d <= 8.  Other shapes return NFN_E_SHAPE (compute t = h W + b and call
+ *   nfn_chain_logprob_f32 instead).  Workspace as for nfn_chain_logprob_f32.
+ */
+int32_t nfn_chain_logprob_dense_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride,
+                                    int32_t H, const float* W, const float* bias, int64_t B, int32_t d,
+                                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                                    const float* y_std, float* out_logp, double* out_sum, double* workspace,
+                                    void* stream);
 
 /*
  * Density on a grid of y values shared by every parameter row:

@@ -34,6 +34,7 @@ UNITS = [
     ("grad_group_fast", "nfn_grad_group.hip", ["-DNFN_FAST=1"]),
     ("grad_group_precise", "nfn_grad_group.hip", ["-DNFN_FAST=0"]),
     ("grid", "nfn_grid.hip", []),
+    ("dense", "nfn_dense.hip", []),
     ("comm", "nfn_comm.hip", []),
 ]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")

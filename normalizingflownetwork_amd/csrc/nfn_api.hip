@@ -362,6 +362,67 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   return check_hip("chain_grad_kernel launch");
 }
 
+int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride, int32_t H, const float* W,
+                  const float* bias, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                  const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
+                  void* stream) {
+  g_last_error.clear();
+  DenseArgs da;
+  memset(&da, 0, sizeof(da));
+  ChainArgs& a = da.c;
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");
+  // the fused kernel's shapes: H a power of two in [4, 64] (16-byte h pieces, 4-wide
+  // MFMA k-steps), P <= 64 (per-wave t tile), d <= 8
+  if (H < 4 || H > 64 || (H & (H - 1)) != 0) return fail(NFN_E_SHAPE, "hidden width H must be 4, 8, 16, 32 or 64");
+  if (P < 1 || P > 64) return fail(NFN_E_SHAPE, "fused dense path needs 1 <= P <= 64");
+  if (d > 8) return fail(NFN_E_SHAPE, "fused dense path needs n_dims <= 8");
+  if (h_rowstride < H || (h_rowstride & 3) != 0) return fail(NFN_E_SHAPE, "h row stride must be >= H and a multiple of 4");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B == 0) {
+    if (out_sum && hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+    return NFN_OK;
+  }
+  if (!y || !h || !W) return fail(NFN_E_NULLPTR, "y, h or W is NULL");
+  if ((reinterpret_cast<uintptr_t>(h) & 15) != 0) return fail(NFN_E_SHAPE, "h must be 16-byte aligned");
+  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
+  if (!out && !workspace) return NFN_OK;
+  a.y = y;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.out = out;
+  a.partials = workspace ? workspace + 1 : nullptr;
+  a.y_bstride = y_bstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = P | 1;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = 1;
+  a.ntiles = (B + 63) / 64;
+  da.h = h;
+  da.h_rowstride = h_rowstride;
+  da.W = W;
+  da.bias = bias;
+  da.H = H;
+  da.h_lds_stride = H | 1;
+  const int NP = ((P + 15) / 16) * 16;
+  const size_t lds = (size_t)(H * NP + 4 * (64 * da.h_lds_stride + 64 * a.lds_stride) + 16) * sizeof(float);
+  int64_t grid = 0;
+  if (!launch_dense(use_fast_math(), dm_for(d), H / 4, da, lds, s, &grid))
+    return fail(NFN_E_SHAPE, "no fused dense instance for this shape");
+  int32_t rc = check_hip("chain_dense_kernel launch");
+  if (rc != NFN_OK) return rc;
+  if (out_sum) {
+    launch_reduce_partials((const double*)workspace, out_sum, s);
+    rc = check_hip("reduce_partials_kernel launch");
+  }
+  return rc;
+}
+
 int32_t run_grid(const float* y_grid, int64_t y_gstride, int32_t G, const float* t, int64_t t_rowstride, int64_t B,
                  int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                  const float* y_std, float* out, int64_t out_gstride, void* stream) {
@@ -490,6 +551,15 @@ int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const floa
                                    float* grad_t, int64_t grad_t_rowstride, float* grad_y, void* stream) {
   return run_grad(y, y_bstride, t, t_rowstride, B, d, flow_ids, K, trainable_base, y_mean, y_std, g_out, out_logp,
                   grad_t, grad_t_rowstride, grad_y, stream);
+}
+
+int32_t nfn_chain_logprob_dense_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride,
+                                    int32_t H, const float* W, const float* bias, int64_t B, int32_t d,
+                                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                                    const float* y_std, float* out_logp, double* out_sum, double* workspace,
+                                    void* stream) {
+  return run_dense(y, y_bstride, h, h_rowstride, H, W, bias, B, d, flow_ids, K, trainable_base, y_mean, y_std,
+                   out_logp, out_sum, workspace, stream);
 }
 
 int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32_t G, const float* t,

@@ -1,0 +1,182 @@
+// nfn_dense.hip — the reference's output Dense layer fused into the chain
+// (SURVEY.md §8(f) row 2): t = h W + b (MaximumLikelihoodNNEstimator.py:43, linear
+// activation) is formed on chip from the last hidden activations h (B, H), so the
+// kernel streams 4H bytes of h per sample instead of the 4P bytes of t
+// (C2 with H = 16: 64 B instead of 128 B).
+//
+// Persistent grid, every wave owns a stream of 64-sample tiles.  Per tile:
+//   1. the tile's h rows (prefetched into registers one tile ahead, non-temporal,
+//      coalesced 16-byte pieces) go to the wave's LDS slot at an odd row stride;
+//   2. the 64 x P tile of t is computed with v_mfma_f32_16x16x4_f32 (exact fp32,
+//      = an fmaf chain): A = h from LDS (lane l: row 16 mt + l % 16, k = 4 ks + l / 16),
+//      B = W from the workgroup's LDS copy, four 16-row M tiles per 16-column N tile;
+//      accumulators + bias are written into the wave's t tile (odd stride);
+//   3. the chain runs per lane exactly as in chain_persistent_kernel.
+#include "nfn_launch.h"
+
+namespace nfn {
+namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int DM, bool FAST, int NVH>
+__global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int H = da.H;
+  const int QH = H >> 2;             // float4 pieces per h row (power of two, <= 16)
+  const int SH = da.h_lds_stride;    // odd
+  const int S = a.lds_stride;        // odd, >= P
+  const int P = a.P;
+  const int NN = (P + 15) >> 4;      // 16-column N tiles
+  const int NK = QH;                 // k-steps of 4
+  const int NP = NN * 16;
+  // LDS: [W: H x NP, zero-padded] [per wave: h tile 64 x SH | t tile 64 x S]
+  float* wl = lds;
+  float* hl = lds + H * NP + wid * (64 * SH + 64 * S);
+  float* tl = hl + 64 * SH;
+  for (int i = tid; i < H * NP; i += blockDim.x) {
+    const int k = i / NP, n = i - (i / NP) * NP;
+    wl[i] = n < P ? da.W[(int64_t)k * P + n] : 0.0f;
+  }
+  __syncthreads();
+  const int r0 = lane / QH;
+  const int c4 = lane - r0 * QH;
+  const int rstep = 64 / QH;
+  const int64_t hs = da.h_rowstride;
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  float corr = 0.0f;
+  if (a.y_mean) {
+    for (int j = 0; j < a.d; ++j) corr += f_log<FAST>(a.y_std[j]);
+  }
+
+  float4 buf[NVH];
+  float ybuf[DM];
+  auto issue = [&](int64_t tile) {
+    const int64_t b0 = tile * 64;
+    const int nr = (int)min((int64_t)64, a.B - b0);
+    const float* base = da.h + b0 * hs + 4 * c4;
+#pragma unroll
+    for (int k = 0; k < NVH; ++k)
+      if (r0 + k * rstep < nr) buf[k] = load_row4<true>(base + (int64_t)(r0 + k * rstep) * hs);
+    if (lane < nr) {
+      const float* yr = a.y + (b0 + lane) * a.y_bstride;
+#pragma unroll
+      for (int j = 0; j < DM; ++j) ybuf[j] = j < a.d ? yr[j] : 0.0f;
+    }
+  };
+
+  double acc_sum = 0.0;
+  int64_t tile = u0;
+  if (tile < a.ntiles) issue(tile);
+  for (; tile < a.ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int nr = (int)min((int64_t)64, a.B - b0);
+#pragma unroll
+    for (int k = 0; k < NVH; ++k) {
+      const int r = r0 + k * rstep;
+      float* dst = hl + r * SH + 4 * c4;
+      const float4 v = r < nr ? buf[k] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      dst[0] = v.x;
+      dst[1] = v.y;
+      dst[2] = v.z;
+      dst[3] = v.w;
+    }
+    float z[DM];
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+      z[j] = ybuf[j];
+      if (a.y_mean && j < a.d) z[j] = f_div<FAST>(z[j] - a.y_mean[j], a.y_std[j]);
+    }
+    wave_lds_sync();
+    if (tile + ustep < a.ntiles) issue(tile + ustep);
+    // t = h W + b on the matrix cores, 16 columns at a time
+    const int am = lane & 15;      // A row within an M tile / B and C column
+    const int ak = lane >> 4;      // A column (k) within a k-step / B row / C row quad
+    for (int nt = 0; nt < NN; ++nt) {
+      f32x4v acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int ks = 0; ks < NK; ++ks) {
+        const float bv = wl[(4 * ks + ak) * NP + 16 * nt + am];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const float av = hl[(16 * mt + am) * SH + 4 * ks + ak];
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mt], 0, 0, 0);
+        }
+      }
+      const int n = 16 * nt + am;
+      if (n < P) {
+        const float bn = da.bias ? da.bias[n] : 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tl[(16 * mt + 4 * ak + i) * S + n] = acc[mt][i] + bn;
+        }
+      }
+    }
+    wave_lds_sync();
+    if (lane < nr) {
+      const float* row = tl + lane * S;
+      float lp;
+      if constexpr (DM == 1 && FAST)
+        lp = (a.prog.K <= 16 ? eval_chain1_fast<true>(z[0], row, a) : eval_chain1_fast<false>(z[0], row, a)) - corr;
+      else
+        lp = eval_chain<DM, FAST>(z, row, a) - corr;
+      if (a.out) __builtin_nontemporal_store(lp, a.out + b0 + lane);
+      acc_sum += (double)lp;
+    }
+    wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
+  }
+  if (a.partials) {
+    const double sum = block_sum(acc_sum, red);
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
+
+template <int DM, bool FAST, int NVH>
+void launch_d(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = chain_dense_kernel<DM, FAST, NVH>;
+  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+}
+
+template <int DM, bool FAST>
+bool launch_d_h(int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* g) {
+  switch (nvh) {
+    case 1: launch_d<DM, FAST, 1>(da, lds, s, g); return true;
+    case 2: launch_d<DM, FAST, 2>(da, lds, s, g); return true;
+    case 4: launch_d<DM, FAST, 4>(da, lds, s, g); return true;
+    case 8: launch_d<DM, FAST, 8>(da, lds, s, g); return true;
+    case 16: launch_d<DM, FAST, 16>(da, lds, s, g); return true;
+  }
+  return false;
+}
+
+template <bool FAST>
+bool launch_d_dm(int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* g) {
+  switch (dm) {
+    case 1: return launch_d_h<1, FAST>(nvh, da, lds, s, g);
+    case 2: return launch_d_h<2, FAST>(nvh, da, lds, s, g);
+    case 4: return launch_d_h<4, FAST>(nvh, da, lds, s, g);
+    case 8: return launch_d_h<8, FAST>(nvh, da, lds, s, g);
+  }
+  return false;
+}
+
+}  // namespace
+
+bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid) {
+  return fast ? launch_d_dm<true>(dm, nvh, da, lds, s, grid) : launch_d_dm<false>(dm, nvh, da, lds, s, grid);
+}
+
+}  // namespace nfn

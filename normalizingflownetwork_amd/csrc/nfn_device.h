@@ -98,6 +98,17 @@ struct ChainArgs {
   FlowProgram prog;
 };
 
+// Output Dense layer fused into the chain (nfn_dense.hip): t = h W + b on chip.
+struct DenseArgs {
+  ChainArgs c;           // t / t_rowstride unused
+  const float* h;        // (B, H) rows at h_rowstride floats
+  int64_t h_rowstride;
+  const float* W;        // (H, P) row-major
+  const float* bias;     // (P,) or NULL
+  int32_t H;
+  int32_t h_lds_stride;  // odd, > H
+};
+
 // Density grid (nfn_grid.hip): y values shared by all parameter rows.
 struct GridArgs {
   ChainArgs c;

@@ -62,6 +62,8 @@ bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_
 bool launch_grad_group_fast(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s,
                                int64_t* grid);
+// nfn_dense.hip; false if (dm, H) has no instance
+bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
 // nfn_grid.hip
 void launch_grid(bool fast, int dm, const GridArgs& ga, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_misc.hip

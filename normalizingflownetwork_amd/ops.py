@@ -219,6 +219,99 @@ def log_prob(y, t, flow_types: Sequence[str], n_dims: int, trainable_base: bool,
     return _ChainLogProb.apply(y, t, tuple(flow_types), int(n_dims), bool(trainable_base), y_mean, y_std)
 
 
+DENSE_HIDDEN_WIDTHS = (4, 8, 16, 32, 64)
+
+
+def dense_fusable(H: int, P: int, n_dims: int) -> bool:
+    """Shapes the fused Dense->chain kernel takes (include/nfn.h, nfn_chain_logprob_dense_f32)."""
+    return H in DENSE_HIDDEN_WIDTHS and 1 <= P <= 64 and n_dims <= 8
+
+
+def chain_log_prob_dense(
+    y,
+    h,
+    W,
+    b,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+    want_values: bool = True,
+    want_sum: bool = False,
+):
+    """``log_prob(y | t = h W + b)`` with the estimator's output Dense layer
+    (``MaximumLikelihoodNNEstimator.py:37-44``) fused into the chain kernel: ``h`` (B, H) last
+    hidden activations, ``W`` (H, P), ``b`` (P,).  Shapes the fused kernel does not take run
+    as a library GEMM (torch) followed by the chain kernel."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    h = as_device_f32(h, dev)
+    assert h.dim() == 2, "h must be (B, H)"
+    H = int(h.shape[1])
+    W = as_device_f32(W, dev).contiguous()
+    assert tuple(W.shape) == (H, P), f"W must be ({H}, {P})"
+    bb = None if b is None else as_device_f32(b, dev).reshape(-1).contiguous()
+    if not dense_fusable(H, P, n_dims) or h.stride(0) % 4 or h.data_ptr() % 16:
+        t = h @ W + (bb if bb is not None else 0.0)
+        return chain_log_prob(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, want_values, want_sum)
+    y = _prep_2d(y, n_dims, "y", dev)
+    B = int(h.shape[0])
+    assert y.shape[0] in (1, B), "incompatible batch sizes"
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
+    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    lib = _lib.load()
+    ws = _workspace(int(lib.nfn_chain_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
+    ids, k = flow_ids(flow_types)
+    rc = lib.nfn_chain_logprob_dense_f32(
+        _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), H, _ptr(W), _ptr(bb), B, int(n_dims),
+        ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys), _ptr(out), _ptr(osum),
+        _ptr(ws), _stream(),
+    )
+    _lib.check(rc, "nfn_chain_logprob_dense_f32")
+    return out, osum
+
+
+class DenseLauncher:
+    """Pre-bound fused Dense->chain launch over fixed device buffers (benchmark loop)."""
+
+    def __init__(self, y: torch.Tensor, h: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor],
+                 flow_types: Sequence[str], n_dims: int, trainable_base: bool, write_values: bool = True):
+        self.lib = _lib.load()
+        dev = y.device
+        self.n_dims = int(n_dims)
+        self.P = total_param_size(flow_types, n_dims, trainable_base)
+        self.B, self.H = int(h.shape[0]), int(h.shape[1])
+        assert dense_fusable(self.H, self.P, self.n_dims) and h.stride(1) == 1 and tuple(W.shape) == (self.H, self.P)
+        self.y, self.h, self.W, self.b = y, h, W.contiguous(), b
+        self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
+        self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
+        self.partials = torch.empty((max(1, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
+                                    dtype=torch.float64, device=dev)
+        self._ids, self._k = flow_ids(flow_types)
+        self._args = (
+            _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), self.H, _ptr(self.W), _ptr(b), self.B, self.n_dims,
+            ctypes.cast(self._ids, ctypes.c_void_p), self._k, int(bool(trainable_base)), None, None, _ptr(self.out),
+            None, _ptr(self.partials),
+        )
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self.lib.nfn_chain_logprob_dense_f32(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_chain_logprob_dense_f32")
+
+    def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
+        rc = self.lib.nfn_reduce_partials_f64(_ptr(self.partials), _ptr(self.sum),
+                                              stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_reduce_partials_f64")
+        return self.sum
+
+
 def chain_log_prob_grid(
     y_grid,
     t,

@@ -139,3 +139,18 @@ def test_grid_entry_point_validates(native_lib):
     assert f(None, 1, -1, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 10, None) == _lib.NFN_E_SHAPE
     assert f(None, 1, 4, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 9, None) == _lib.NFN_E_SHAPE
     assert f(None, 1, 0, None, 8, 10, 1, p_ids, 2, 1, None, None, None, 10, None) == _lib.NFN_OK
+
+
+def test_dense_entry_point_validates(native_lib):
+    from normalizingflownetwork_amd import _lib
+
+    ids = _ids("planar", "radial")
+    p_ids = ctypes.cast(ids, ctypes.c_void_p)
+    f = native_lib.nfn_chain_logprob_dense_f32
+    args = lambda H, hs, d=1: (None, 1, None, hs, H, None, None, 10, d, p_ids, 2, 1, None, None, None, None,  # noqa: E731
+                               None, None)
+    assert f(*args(16, 16)) == _lib.NFN_E_NULLPTR
+    assert f(*args(10, 12)) == _lib.NFN_E_SHAPE       # H not a power of two
+    assert f(*args(16, 8)) == _lib.NFN_E_SHAPE        # row stride < H
+    assert f(*args(16, 18)) == _lib.NFN_E_SHAPE       # row stride not a multiple of 4
+    assert "dense" in _lib.last_error() or "stride" in _lib.last_error()
