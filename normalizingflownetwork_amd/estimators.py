@@ -67,6 +67,14 @@ class _MLP:
                 h = act(h)
         return h
 
+    def hidden(self, x: torch.Tensor) -> torch.Tensor:
+        """Activations entering the linear output layer (the fused Dense path's input)."""
+        act = _ACTIVATIONS[self.activation]
+        h = x
+        for w, b in zip(self.weights[:-1], self.biases[:-1]):
+            h = act(h @ w + b)
+        return h.contiguous()
+
 
 class BaseEstimator:
     """Evaluation half of ``estimators/BaseEstimator.py``."""
@@ -124,6 +132,24 @@ class BaseEstimator:
     def __call__(self, x):
         return self.dist_layer(self.params(x))
 
+    def _fused_dense_inputs(self, x):
+        """``(h, W, b)`` of the output Dense layer when the fused Dense->chain kernel takes
+        the shapes (evaluation only: no autograd through it), else None."""
+        if torch.is_grad_enabled() and any(w.requires_grad for w in (self._mlp.weights if self._mlp else [])):
+            return None
+        x = ops.as_device_f32(x)
+        if x.dim() == 1:
+            x = x.unsqueeze(-1)
+        if self._mlp is None:
+            self._build(int(x.shape[-1]))
+        self._mlp.to(x.device)
+        W, b = self._mlp.weights[-1], self._mlp.biases[-1]
+        if not ops.dense_fusable(int(W.shape[0]), int(W.shape[1]), self.n_dims) or len(self._mlp.weights) < 2:
+            return None
+        xm = torch.as_tensor(self.x_mean, dtype=torch.float32, device=x.device)
+        xs = torch.as_tensor(self.x_std, dtype=torch.float32, device=x.device)
+        return self._mlp.hidden((x - xm) / (xs + 1e-8)), W, b
+
     def call(self, x, training=False):
         return self(x)
 
@@ -133,6 +159,12 @@ class BaseEstimator:
         x = np.asarray(x, np.float32) if not isinstance(x, torch.Tensor) else x
         y = np.asarray(y, np.float32) if not isinstance(y, torch.Tensor) else y
         assert tuple(x.shape) == tuple(y.shape)
+        fused = self._fused_dense_inputs(x)
+        if fused is not None:  # output Dense layer fused into the chain kernel
+            dl = self.dist_layer
+            lp, _ = ops.chain_log_prob_dense(y, *fused, dl.flow_types, self.n_dims, dl.trainable_base_dist,
+                                             self.y_mean, self.y_std)
+            return lp
         output = self(x)
         assert output.event_shape == y.shape[-1]
         return output.log_prob(y, self.y_mean, self.y_std)
@@ -145,6 +177,12 @@ class BaseEstimator:
         """``BaseEstimator.py:43-47``: mean log-likelihood, reduced on the device in fp64."""
         x_data = np.asarray(x_data, np.float32) if not isinstance(x_data, torch.Tensor) else x_data
         y_data = np.asarray(y_data, np.float32) if not isinstance(y_data, torch.Tensor) else y_data
+        fused = self._fused_dense_inputs(x_data)
+        if fused is not None:  # output Dense layer fused into the chain kernel
+            dl = self.dist_layer
+            _, s = ops.chain_log_prob_dense(y_data, *fused, dl.flow_types, self.n_dims, dl.trainable_base_dist,
+                                            self.y_mean, self.y_std, want_values=False, want_sum=True)
+            return float(s.item()) / int(y_data.shape[0])
         output = self(x_data)
         s = output.log_prob_sum(y_data, self.y_mean, self.y_std)
         return float(s.item()) / int(y_data.shape[0])
