@@ -42,6 +42,9 @@
  *                             log_prob: MaximumLikelihoodNNEstimator.py:37-44 (Dense(P)) +
  *                             DistributionLayers.py:245-255, i.e. model(x).log_prob(y) given the
  *                             last hidden activations
+ *   nfn_chain_sample_f32   <- new capability: the reference's layer cannot sample (its flows have
+ *                             no _inverse; DistributionLayers.py:223-226, 240); this draws
+ *                             y ~ p(y | t) through the inverted flows
  *   nfn_chain_logprob_grid_f32
  *                          <- the per-grid-point loop of dist.prob(y[i]) over a batch of x in
  *                             evaluation/visualization/flow_plotting.py:33-53 (plot_model)
@@ -161,6 +164,18 @@ int32_t nfn_chain_logprob_dense_f32(const float* y, int64_t y_bstride, const flo
                                     const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                                     const float* y_std, float* out_logp, double* out_sum, double* workspace,
                                     void* stream);
+
+/*
+ * Sampling: y_b = f_0^{-1}(... f_{K-1}^{-1}(loc_b + scale_b * eps_b)) [* y_std + y_mean]
+ * for caller-supplied standard-normal eps (B, d) at eps_bstride (0 = one row);
+ * planar steps are inverted by safeguarded Newton iteration (the constraint
+ * w.u_hat >= -1 + 1e-5 makes them invertible), radial steps in closed form.
+ *   y_out    : (B, d) contiguous
+ *   logp_out : (B,) log-density of each sample (incl. -sum log y_std), or NULL
+ */
+int32_t nfn_chain_sample_f32(const float* eps, int64_t eps_bstride, const float* t, int64_t t_rowstride, int64_t B,
+                             int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                             const float* y_mean, const float* y_std, float* y_out, float* logp_out, void* stream);
 
 /*
  * Density on a grid of y values shared by every parameter row:

@@ -53,6 +53,10 @@ SIGNATURES = {
         [_vp, _c_int64, _vp, _c_int64, _c_int32, _vp, _vp, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp,
          _vp, _vp, _vp, _vp],
     ),
+    "nfn_chain_sample_f32": (
+        _c_int32,
+        [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp, _vp, _vp],
+    ),
     "nfn_chain_logprob_grid_f32": (
         _c_int32,
         [_vp, _c_int64, _c_int32, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp,

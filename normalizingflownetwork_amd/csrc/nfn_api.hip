@@ -423,6 +423,48 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   return rc;
 }
 
+int32_t run_sample(const float* eps, int64_t eps_bstride, const float* t, int64_t t_rowstride, int64_t B, int32_t d,
+                   const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                   const float* y_std, float* y_out, float* logp_out, void* stream) {
+  g_last_error.clear();
+  SampleArgs sa;
+  memset(&sa, 0, sizeof(sa));
+  ChainArgs& a = sa.c;
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (eps_bstride < 0 || (eps_bstride != 0 && eps_bstride < d)) return fail(NFN_E_SHAPE, "bad eps batch stride");
+  if (t_rowstride < 0 || (t_rowstride != 0 && t_rowstride < P)) return fail(NFN_E_SHAPE, "bad t row stride");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  if (B == 0) return NFN_OK;
+  if (!eps || !y_out) return fail(NFN_E_NULLPTR, "eps or y_out is NULL");
+  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
+  const TileGeom g = tile_geom(P);
+  if ((size_t)g.rows * ((size_t)g.lds_stride * sizeof(float)) > (size_t)kLdsMaxBytes)
+    return fail(NFN_E_SHAPE, "parameter row too wide for LDS");
+  a.t = t;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.t_rowstride = t_rowstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = g.lds_stride;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = 1;
+  a.vec4 = ((P & 3) == 0) && ((t_rowstride & 3) == 0) && ((reinterpret_cast<uintptr_t>(t) & 15) == 0);
+  a.tile_rows = g.rows;
+  sa.eps = eps;
+  sa.eps_bstride = eps_bstride;
+  sa.y_out = y_out;
+  sa.logp = logp_out;
+  const int64_t nblk = (B + g.rows - 1) / g.rows;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  launch_sample(use_fast_math(), dm_for(d), sa, dim3((unsigned)nblk), dim3((unsigned)g.threads), g.lds_bytes,
+                reinterpret_cast<hipStream_t>(stream));
+  return check_hip("chain_sample_kernel launch");
+}
+
 int32_t run_grid(const float* y_grid, int64_t y_gstride, int32_t G, const float* t, int64_t t_rowstride, int64_t B,
                  int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                  const float* y_std, float* out, int64_t out_gstride, void* stream) {
@@ -560,6 +602,13 @@ int32_t nfn_chain_logprob_dense_f32(const float* y, int64_t y_bstride, const flo
                                     void* stream) {
   return run_dense(y, y_bstride, h, h_rowstride, H, W, bias, B, d, flow_ids, K, trainable_base, y_mean, y_std,
                    out_logp, out_sum, workspace, stream);
+}
+
+int32_t nfn_chain_sample_f32(const float* eps, int64_t eps_bstride, const float* t, int64_t t_rowstride, int64_t B,
+                             int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                             const float* y_mean, const float* y_std, float* y_out, float* logp_out, void* stream) {
+  return run_sample(eps, eps_bstride, t, t_rowstride, B, d, flow_ids, K, trainable_base, y_mean, y_std, y_out,
+                    logp_out, stream);
 }
 
 int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32_t G, const float* t,

@@ -109,6 +109,15 @@ struct DenseArgs {
   int32_t h_lds_stride;  // odd, > H
 };
 
+// Sampling through the inverted flows (nfn_sample.hip).
+struct SampleArgs {
+  ChainArgs c;
+  const float* eps;      // (B, d) standard-normal draws at eps_bstride floats
+  int64_t eps_bstride;
+  float* y_out;          // (B, d) contiguous
+  float* logp;           // (B,) log-density of each sample, or NULL
+};
+
 // Density grid (nfn_grid.hip): y values shared by all parameter rows.
 struct GridArgs {
   ChainArgs c;

@@ -64,6 +64,8 @@ bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_
                                int64_t* grid);
 // nfn_dense.hip; false if (dm, H) has no instance
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
+// nfn_sample.hip
+void launch_sample(bool fast, int dm, const SampleArgs& sa, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_grid.hip
 void launch_grid(bool fast, int dm, const GridArgs& ga, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_misc.hip

@@ -179,10 +179,31 @@ class FlowDistribution:
     def prob_grid(self, y_grid, y_mean=None, y_std=None) -> torch.Tensor:
         return torch.exp(self.log_prob_grid(y_grid, y_mean, y_std))
 
-    def sample(self, *args, **kwargs):
-        raise NotImplementedError(
-            "the inverted flows cannot sample (reference DistributionLayers.py:223-226, 240)"
-        )
+    def sample(self, sample_shape=(), seed=None) -> torch.Tensor:
+        """Draws of shape ``sample_shape + batch_shape + [d]`` through the inverted flows
+        (``nfn_chain_sample_f32``).  An extension: the reference's layer cannot sample
+        (``DistributionLayers.py:223-226, 240``) because its flows define no inverse."""
+        return self.sample_and_log_prob(sample_shape, seed)[0]
+
+    def sample_and_log_prob(self, sample_shape=(), seed=None):
+        d = self._n_dims
+        P = _shape(self._t)[-1]
+        t = ops.as_device_f32(self._t) if P > 0 else None
+        bshape = tuple(self.batch_shape)
+        sshape = (sample_shape,) if isinstance(sample_shape, int) else tuple(sample_shape)
+        n_s = int(np.prod(sshape)) if sshape else 1
+        nb = int(np.prod(bshape)) if bshape else 1
+        dev = ops._device()
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(int(seed) if seed is not None else int(torch.randint(0, 2**62, (1,)).item()))
+        eps = torch.randn((n_s * nb, d), generator=gen, device=dev)
+        if t is not None:
+            t2 = t.reshape(nb, P)
+            t2 = t2.repeat(n_s, 1) if n_s > 1 else t2
+        else:
+            t2 = torch.zeros((1, 0), dtype=torch.float32, device=dev)
+        y, lp = ops.chain_sample(eps, t2, self._flow_types, d, self._trainable)
+        return y.reshape(sshape + bshape + (d,)), lp.reshape(sshape + bshape)
 
 
 class InverseNormalizingFlowLayer:

@@ -312,6 +312,33 @@ class DenseLauncher:
         return self.sum
 
 
+def chain_sample(eps, t, flow_types: Sequence[str], n_dims: int, trainable_base: bool, y_mean=None, y_std=None,
+                 want_log_prob: bool = True):
+    """Draw ``y ~ p(y | t)`` through the inverted flows for given standard-normal ``eps``
+    (B or 1, d): returns ``(y (B, d), log_prob (B,) | None)`` (``nfn_chain_sample_f32``).
+    A capability the reference lacks (its flows define no inverse)."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    e = _prep_2d(eps, n_dims, "eps", dev)
+    t = _prep_2d(t, P, "t", dev) if P > 0 else torch.zeros((1, 1), dtype=torch.float32, device=dev)
+    B = max(int(e.shape[0]), int(t.shape[0]) if P > 0 else 1)
+    assert e.shape[0] in (1, B) and (P == 0 or t.shape[0] in (1, B)), "incompatible batch sizes"
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    y = torch.empty((B, n_dims), dtype=torch.float32, device=dev)
+    lp = torch.empty((B,), dtype=torch.float32, device=dev) if want_log_prob else None
+    ids, k = flow_ids(flow_types)
+    rc = _lib.load().nfn_chain_sample_f32(
+        _ptr(e), _row_stride(e), _ptr(t), _row_stride(t) if P > 0 else 0, B, int(n_dims),
+        ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys), _ptr(y), _ptr(lp),
+        _stream(),
+    )
+    _lib.check(rc, "nfn_chain_sample_f32")
+    return y, lp
+
+
 def chain_log_prob_grid(
     y_grid,
     t,

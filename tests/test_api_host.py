@@ -3,6 +3,7 @@ assertion checks of tests/test_flows.py and tests/test_distribution_layers.py,
 re-expressed against normalizingflownetwork_amd."""
 
 import numpy as np
+import torch
 import pytest
 
 from normalizingflownetwork_amd import FLOWS, AffineFlow, InverseNormalizingFlowLayer, PlanarFlow, RadialFlow
@@ -88,12 +89,16 @@ def test_get_bijector_blocks_are_reversed():
     np.testing.assert_array_equal(chain.bijectors[2]._t, [[5, 6, 7]])  # planar (3)
 
 
-def test_sampling_is_impossible():
-    dist = InverseNormalizingFlowLayer(("radial",), 1, False)(np.ones((2, 3), np.float32))
-    with pytest.raises(NotImplementedError):
-        dist.sample()
+def test_bijector_inverse_is_not_defined():
+    """The reference's flows define no _inverse (DistributionLayers.py:223-226); the
+    host mirror keeps that.  Sampling the distribution is this build's extension
+    (nfn_chain_sample_f32) and, like every compute path, needs the GPU."""
     with pytest.raises(NotImplementedError):
         RadialFlow(np.ones((2, 3), np.float32), 1).inverse([[0.0]])
+    dist = InverseNormalizingFlowLayer(("radial",), 1, False)(np.ones((2, 3), np.float32))
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError):
+            dist.sample()
 
 
 def test_tensorshape_semantics():
