@@ -191,12 +191,15 @@ def main():
                          "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient); dense = the "
                          "output Dense layer (H -> P) fused into the chain, streaming h instead of t")
     ap.add_argument("--hidden", type=int, default=16, help="--mode dense: hidden width H")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="initialise the process group and run the all-reduce even at N = 1 (tests)")
     ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
                     help="N > 1 mean all-reduce: torch.distributed, or the library's own RCCL "
                          "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
     args = ap.parse_args()
 
-    rank, world, local_rank = init_from_env(backend=args.backend)
+    rank, world, local_rank = init_from_env(backend=args.backend, force=args.force_pg)
+    dist_on = dist.is_initialized()  # world > 1, or --force-pg (test hook: the N > 1 step path at N = 1)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dev_index = local_rank % max(1, torch.cuda.device_count())
@@ -230,10 +233,16 @@ def main():
         launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
-    red = torch.zeros((2,), dtype=torch.float64, device=dev)
+    # (sum, count) all-reduce buffers: a ring of two, so step i's all-reduce (async, on
+    # the process group's stream) overlaps step i+1's chain kernel; a buffer is reused
+    # only after the stream has waited for its previous all-reduce
+    reds = [torch.zeros((2,), dtype=torch.float64, device=dev) for _ in range(2)]
+    works = [None, None]
+    nstep = [0]
+    red = reds[0]
     evals_per_step = B * (1 if S is None else S)
     native = None
-    if world > 1 and args.allreduce == "native":
+    if dist_on and args.allreduce == "native":
         from normalizingflownetwork_amd.parallel import NativeComm
 
         native = NativeComm()
@@ -249,37 +258,55 @@ def main():
         s = launcher.finish_sum(sh)
         if native is not None:
             native.allreduce_mean(s, B, sh)
-        elif world > 1:
-            red[0:1].copy_(s)
-            red[1] = float(B)
+        elif dist_on:
+            i = nstep[0] % 2
+            nstep[0] += 1
             if args.backend == "nccl":
-                dist.all_reduce(red)
+                if works[i] is not None:
+                    works[i].wait()  # stream-side wait: the buffer's previous all-reduce is done
+                buf = reds[i]
+                buf[0:1].copy_(s)
+                buf[1] = float(B)
+                works[i] = dist.all_reduce(buf, async_op=True)
             else:  # gloo reduces host tensors
-                h = red.cpu()
+                buf = reds[i]
+                buf[0:1].copy_(s)
+                buf[1] = float(B)
+                h = buf.cpu()
                 dist.all_reduce(h)
-                red.copy_(h)
+                buf.copy_(h)
+            last_red[0] = buf
+
+    last_red = [reds[0]]
+
+    def drain():
+        for w in works:
+            if w is not None:
+                w.wait()
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for e0, e1 in evs:
         step(e0, e1)
+    drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    if dist_on:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    if world > 1:
+    if dist_on:
         kt = torch.tensor([kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
@@ -306,7 +333,8 @@ def main():
     elif native is not None:
         mean_ll = float(native.mean.item())
     else:
-        mean_ll = float(red[0].item() / red[1].item()) if world > 1 else float(launcher.sum.item()) / B
+        red = last_red[0]
+        mean_ll = float(red[0].item() / red[1].item()) if dist_on else float(launcher.sum.item()) / B
 
     if rank == 0:
         total_evals = evals_per_step * world * args.steps
@@ -389,7 +417,7 @@ def main():
         print(json.dumps(line), flush=True)
     if native is not None:
         native.close()
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -109,15 +109,21 @@ class NativeComm:
             self.handle = ctypes.c_void_p()
 
 
-def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
+def init_from_env(backend: Optional[str] = None, force: bool = False) -> Tuple[int, int, int]:
     """Initialise the default process group from torchrun's env (RANK, WORLD_SIZE,
-    LOCAL_RANK, MASTER_ADDR/PORT).  Returns ``(rank, world, local_rank)``."""
+    LOCAL_RANK, MASTER_ADDR/PORT) when there is more than one rank (or ``force``).
+    Returns ``(rank, world, local_rank)``."""
     import os
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if force and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":

@@ -8,6 +8,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from conftest import REPO
@@ -36,3 +37,18 @@ def test_bench_two_ranks_gloo(gpu):
     assert out["value"] > 0 and out["scaling"] == "weak"
     # the all-reduced mean covers both ranks' shards (different seeds => finite mean)
     assert out["mean_log_prob"] == out["mean_log_prob"]
+
+
+@pytest.mark.parametrize("allreduce", ["torch", "native"])
+def test_bench_nccl_step_path_one_rank(gpu, allreduce):
+    """The N > 1 step path over RCCL (async all-reduce ring / the library's own
+    communicator) exercised with one rank on the one GPU of the test box."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "1", "--steps", "5", "--warmup", "2", "--backend", "nccl", "--force-pg",
+           "--allreduce", allreduce, "--batch", str(1 << 18), "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["n_gpus"] == 1 and np.isfinite(out["mean_log_prob"])
