@@ -337,7 +337,7 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   if (dm >= 4 && a.vec4 && t_rowstride != 0 && Q >= 1 && (!grad_t || ga.gt_vec4) &&
       env_int("NFN_GRAD_GROUP", 1) != 0) {
     int G = 4, DPL = 1;
-    group_shape(dm, 0, &G, &DPL);
+    group_shape(dm, env_int("NFN_GROUP_LANES", 0), &G, &DPL);
     const int Rg = 64 / G;
     const int nv = (Q + G - 1) / G;  // float4 slots per lane: (R rows x Q) / 64
     a.lds_stride = group_lds_stride(P, G);
@@ -353,7 +353,12 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   }
   if (wave_ok) {
     a.ntiles = (B + 63) / 64;
-    const int wpb = slot * 4 <= (size_t)80 * 1024 ? 4 : (slot * 2 <= (size_t)80 * 1024 ? 2 : 1);
+    // two waves per workgroup measured fastest on C2 (finer LDS allocation granules
+    // than 4-wave groups at ~11 KB of LDS per wave); NFN_GRAD_WPB overrides (1, 2, 4)
+    int wpb = slot * 2 <= (size_t)80 * 1024 ? 2 : 1;
+    const int want_wpb = env_int("NFN_GRAD_WPB", 0);
+    if (want_wpb == 1 || want_wpb == 2 || want_wpb == 4)
+      wpb = slot * want_wpb <= (size_t)80 * 1024 ? want_wpb : 1;
     int64_t grid = 0;
     if (launch_grad_wave(use_fast_math(), dm, Q, ga, slot * wpb, wpb, s, &grid))
       return check_hip("chain_grad_wave_kernel launch");

@@ -135,8 +135,8 @@ __global__ void __launch_bounds__(64) chain_grad_kernel(GradArgs ga) {
 // registers (non-temporal) while the current tile runs forward + reverse; the
 // gradient tile is then written back from LDS with coalesced non-temporal
 // float4 stores (lane -> (row, 16-byte column) as for the loads).
-template <int DM, bool FAST, int NV>
-__global__ void __launch_bounds__(kMaxBlock) chain_grad_wave_kernel(GradArgs ga) {
+template <int DM, bool FAST, int NV, int MINW>
+__global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradArgs ga) {
   const ChainArgs& a = ga.c;
   extern __shared__ float lds[];
   const int S = a.lds_stride;
@@ -242,7 +242,11 @@ void launch_grad_t(int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_
 
 template <int DM, bool FAST, int NV>
 bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, hipStream_t s, int64_t* grid) {
-  auto k = chain_grad_wave_kernel<DM, FAST, NV>;
+  // tuning knob: NFN_GRAD_CAP=1 caps registers at 4 waves per SIMD (d = 1, 8 float4 / lane)
+  auto k = chain_grad_wave_kernel<DM, FAST, NV, 1>;
+  if constexpr (DM == 1 && NV == 8) {
+    if (env_int("NFN_GRAD_CAP", 0) == 1) k = chain_grad_wave_kernel<DM, FAST, NV, 4>;
+  }
   const int T = 64 * waves_per_block;
   const int64_t teams = persistent_grid(k, T, lds_block, (ga.c.ntiles + waves_per_block - 1) / waves_per_block);
   *grid = std::max<int64_t>(1, teams);

@@ -260,6 +260,10 @@ bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_
   if (G == 4 && DPL == 2) return launch_gg_nv<4, 2>(nv, ga, lds, s, grid);
   if (G == 4 && DPL == 4) return launch_gg_nv<4, 4>(nv, ga, lds, s, grid);
   if (G == 8 && DPL == 4) return launch_gg_nv<8, 4>(nv, ga, lds, s, grid);
+  if constexpr (kFast) {  // alternates for tuning runs (NFN_GROUP_LANES=8)
+    if (G == 8 && DPL == 1) return launch_gg_nv<8, 1>(nv, ga, lds, s, grid);
+    if (G == 8 && DPL == 2) return launch_gg_nv<8, 2>(nv, ga, lds, s, grid);
+  }
   return false;
 }
 

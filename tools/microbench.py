@@ -116,15 +116,41 @@ def run_grad(cfg, variants, reps=10, rounds=3):
 
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "ceiling":  # HBM ceilings of plain torch streams over the C2 parameter buffer
+        B, P = 1 << 24, 32
+        t = torch.randn((B, P), device="cuda")
+        out = torch.empty_like(t)
+        stream = torch.cuda.current_stream()
+        for name, fn, nbytes in (("sum_read", lambda: t.sum(), t.numel() * 4),
+                                 ("copy", lambda: out.copy_(t), 2 * t.numel() * 4),
+                                 ("fill_write", lambda: out.fill_(1.0), t.numel() * 4)):
+            for _ in range(3):
+                fn()
+            ms = []
+            for _ in range(3):
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+                for e0, e1 in evs:
+                    e0.record(stream)
+                    fn()
+                    e1.record(stream)
+                torch.cuda.synchronize()
+                ms.append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+            m = float(np.median(ms))
+            print(json.dumps({"variant": name, "ms": m, "GBps": nbytes / m / 1e6, "frac8TBs": nbytes / m / 1e6 / 8000}),
+                  flush=True)
+        return
     if which[0] == "grad":
         v = [{"name": "wave", "env": {}},
+             {"name": "wpb4", "env": {"NFN_GRAD_WPB": 4}},
+             {"name": "wpb1", "env": {"NFN_GRAD_WPB": 1}},
              {"name": "tile_v1", "env": {"NFN_GRAD_WAVE": 0}},
              {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
              {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
              {"name": "v1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_GRAD_WAVE": 0}},
              {"name": "v1_compute_only", "env": {"NFN_ABLATE_LOADS": 1, "NFN_GRAD_WAVE": 0}}]
         run_grad("C2", v)
-        run_grad("C3", [{"name": "group", "env": {}}, {"name": "tile_v1", "env": {"NFN_GRAD_GROUP": 0}},
+        run_grad("C3", [{"name": "group", "env": {}}, {"name": "g8x1", "env": {"NFN_GROUP_LANES": 8}},
+                        {"name": "tile_v1", "env": {"NFN_GRAD_GROUP": 0}},
                         {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                         {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}])
         return
