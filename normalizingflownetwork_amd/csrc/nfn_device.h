@@ -95,6 +95,7 @@ struct ChainArgs {
   int32_t dps;         // posterior: draws per range
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
+  int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
   FlowProgram prog;
 };
 
@@ -805,6 +806,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = sb; s < se; ++s) {
       if (wg_sync) __syncthreads();  // previous unit's LDS rows fully consumed
+      if (a.prio) __builtin_amdgcn_s_setprio(2);  // tuning: hand-off + next prefetch at high priority
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         if (k < Q && r0 + k * rstep < nr) {
@@ -835,6 +837,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
         range_of(unit + ustep, nb, ne);
         issue(unit + ustep, nb, true);
       }
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
       if (lt < nr) {
         float z[DM];
 #pragma unroll
@@ -1258,6 +1261,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     }
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = 0; s < ndraw; ++s) {
+      if (a.prio) __builtin_amdgcn_s_setprio(2);
       {
         int r = r00, c = c00;
 #pragma unroll
@@ -1295,6 +1299,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
         issue(tile, s + 1);
       else if (tile + ustep < a.ntiles)
         issue(tile + ustep, 0);
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
       if (sl < nr) {
         float z[DPL];
 #pragma unroll

@@ -182,6 +182,7 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
   for (; tile < ntiles; tile += ustep) {
     const int64_t b0 = tile * 64;
     const int nr = (int)min((int64_t)64, a.B - b0);
+    if (a.prio) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       if (r0 + k * rstep < nr) {
@@ -205,6 +206,7 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
     const float gl = gbuf;
     wave_lds_sync();
     if (tile + ustep < ntiles) issue(tile + ustep);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
     if (lane < nr) {
       const int64_t b = b0 + lane;
       float adj[DM];

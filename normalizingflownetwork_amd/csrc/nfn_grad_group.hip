@@ -92,6 +92,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
   for (; tile < a.ntiles; tile += ustep) {
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
+    if (a.prio) __builtin_amdgcn_s_setprio(2);
     {
       int r = r00, c = c00;
 #pragma unroll
@@ -125,6 +126,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
     const float gl = gbuf;
     wave_lds_sync();
     if (tile + ustep < a.ntiles) issue(tile + ustep);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
     if (sl < nr) {
       float* row = tl + sl * S;
       // forward, keeping each flow's input

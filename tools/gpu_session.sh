@@ -78,6 +78,7 @@ for s in $STEPS; do
     c3micro) run c3micro 300 python tools/microbench.py c3 ;;
     dense) run bench_dense 300 python bench.py --mode dense --steps 50 --warmup 10 --cpu-seconds 6 ;;
     densetests) run densetests 300 python -m pytest tests/test_gpu_dense.py -m gpu -q -p no:cacheprovider ;;
+    prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
     pf2) run pf2 300 python tools/microbench.py pf2 ;;

@@ -177,6 +177,14 @@ def main():
              {"name": "depth2_wg4", "env": {"NFN_PREFETCH2": 1, "NFN_WG_PER_CU": 4}}]
         run("C2", v)
         return
+    if which[0] == "prio":  # wave priority around the tile hand-off
+        v = [{"name": "prio", "env": {"NFN_PRIO": 1}}, {"name": "noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "prio2", "env": {"NFN_PRIO": 1}}, {"name": "noprio2", "env": {"NFN_PRIO": 0}}]
+        for cfg in ("C2", "C5", "C3"):
+            run(cfg, v, reps=30, rounds=4)
+        run_grad("C2", v)
+        run_grad("C3", v)
+        return
     if which[0] == "valu":  # compute vs memory floors
         for cfg in ("C2", "C5"):
             W = {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}
