@@ -170,7 +170,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
   a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
-  a.prio = env_int("NFN_PRIO", 1) == 1 ? 1 : 0;  // measured +1-2% (C2, C5)
+  a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // measured +1-2% (C2, C5); 2 = + static split
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
   if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");

@@ -806,7 +806,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     float m = -INFINITY, accl = 0.0f, lp = 0.0f;
     for (int s = sb; s < se; ++s) {
       if (wg_sync) __syncthreads();  // previous unit's LDS rows fully consumed
-      if (a.prio) __builtin_amdgcn_s_setprio(2);  // tuning: hand-off + next prefetch at high priority
+      if (a.prio) __builtin_amdgcn_s_setprio(3);  // tuning: hand-off + next prefetch at high priority
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         if (k < Q && r0 + k * rstep < nr) {
@@ -837,7 +837,8 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
         range_of(unit + ustep, nb, ne);
         issue(unit + ustep, nb, true);
       }
-      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      if (a.prio == 2 && (wid & 1)) __builtin_amdgcn_s_setprio(1);  // static: odd waves compute first
+      else if (a.prio) __builtin_amdgcn_s_setprio(0);
       if (lt < nr) {
         float z[DM];
 #pragma unroll

@@ -178,12 +178,12 @@ def main():
         run("C2", v)
         return
     if which[0] == "prio":  # wave priority around the tile hand-off
-        v = [{"name": "prio", "env": {"NFN_PRIO": 1}}, {"name": "noprio", "env": {"NFN_PRIO": 0}},
-             {"name": "prio2", "env": {"NFN_PRIO": 1}}, {"name": "noprio2", "env": {"NFN_PRIO": 0}}]
-        for cfg in ("C2", "C5", "C3"):
+        v = [{"name": "prio", "env": {"NFN_PRIO": 1}}, {"name": "static", "env": {"NFN_PRIO": 2}},
+             {"name": "noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "prio_b", "env": {"NFN_PRIO": 1}}, {"name": "static_b", "env": {"NFN_PRIO": 2}},
+             {"name": "noprio_b", "env": {"NFN_PRIO": 0}}]
+        for cfg in ("C2", "C5"):
             run(cfg, v, reps=30, rounds=4)
-        run_grad("C2", v)
-        run_grad("C3", v)
         return
     if which[0] == "valu":  # compute vs memory floors
         for cfg in ("C2", "C5"):
