@@ -882,91 +882,6 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
   }
 }
 
-// d = 1 plain chain, wave tiles, prefetch depth 2: every wave keeps its next TWO
-// 64-row tiles in flight in registers (bufA / bufB alternate), trading one wave
-// per SIMD of occupancy for twice the bytes in flight per wave.
-template <int NV>
-__global__ void __launch_bounds__(kMaxBlock, 3) chain_wave2_kernel(ChainArgs a) {
-  extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
-  const int T = blockDim.x;
-  const int tid = threadIdx.x;
-  const int Q = a.P >> 2;
-  const int S = a.lds_stride;
-  const int64_t rs = a.t_rowstride;
-  const int wid = tid >> 6;
-  const int lt = tid & 63;
-  float* tl = lds + wid * 64 * S;
-  const int r0 = lt / Q;
-  const int c4 = lt - (lt / Q) * Q;
-  const int rstep = 64 / Q;
-  const int64_t g0 = (int64_t)r0 * rs + 4 * c4;
-  const int64_t gstep = (int64_t)rstep * rs;
-  const int l0 = r0 * S + 4 * c4;
-  const int lstep = rstep * S;
-  const int64_t nunits = a.ntiles;
-  const int64_t u0 = (int64_t)blockIdx.x * (T >> 6) + wid;
-  const int64_t ustep = (int64_t)gridDim.x * (T >> 6);
-
-  float4 bufA[NV], bufB[NV];
-  float yA = 0.0f, yB = 0.0f;
-  auto issue = [&](int64_t unit, float4 (&buf)[NV], float& yv) {
-    if (unit >= nunits) return;
-    const int64_t b0 = unit * 64;
-    const int nr = (int)min((int64_t)64, a.B - b0);
-    const float* base = a.t + b0 * rs;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      if (k < Q && r0 + k * rstep < nr) buf[k] = load_row4<true>(base + g0 + k * gstep);
-    }
-    if (lt < nr) yv = a.y[(b0 + lt) * a.y_bstride];
-  };
-  double acc = 0.0;
-  int64_t pend_b = -1;
-  float pend_v = 0.0f;
-  auto process = [&](int64_t unit, float4 (&buf)[NV], float& yv) {
-    const int64_t b0 = unit * 64;
-    const int nr = (int)min((int64_t)64, a.B - b0);
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      if (k < Q && r0 + k * rstep < nr) {
-        float* dst = tl + l0 + k * lstep;
-        dst[0] = buf[k].x;
-        dst[1] = buf[k].y;
-        dst[2] = buf[k].z;
-        dst[3] = buf[k].w;
-      }
-    }
-    const float z0 = yv;
-    wave_lds_sync();
-    if (pend_b >= 0) {
-      if (a.out) __builtin_nontemporal_store(pend_v, a.out + pend_b);
-      pend_b = -1;
-    }
-    issue(unit + 2 * ustep, buf, yv);  // refill this buffer two units ahead
-    if (lt < nr) {
-      const float lp = eval_chain1_fast<true>(z0, tl + lt * S, a);
-      pend_b = b0 + lt;
-      pend_v = lp;
-      acc += (double)lp;
-    }
-    wave_lds_sync();
-  };
-  issue(u0, bufA, yA);
-  issue(u0 + ustep, bufB, yB);
-  for (int64_t unit = u0; unit < nunits; unit += 2 * ustep) {
-    process(unit, bufA, yA);
-    if (unit + ustep < nunits) process(unit + ustep, bufB, yB);
-  }
-  if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
-  if (a.partials) {
-    const double sum = block_sum(acc, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
-  }
-}
 
 // Combines the per-range (max, scaled sum) pairs of a draw-split posterior:
 // out[b] = M + log(sum_r acc_r * exp(m_r - M)) - log S, M = max_r m_r.

@@ -13,16 +13,6 @@ constexpr bool kFast = NFN_FAST != 0;
 
 template <int DM, int NV, bool POST>
 void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
-  if constexpr (DM == 1 && kFast && !POST && NV == 8) {
-    // experimental depth-2 prefetch (NFN_PREFETCH2=1): d = 1, packed, wave tiles
-    if (env_int("NFN_PREFETCH2", 0) == 1 && a.ownrow == 2 && a.prog.K <= 16 && a.y_mean == nullptr) {
-      auto k2 = chain_wave2_kernel<NV>;
-      const int64_t grid = persistent_grid(k2, T, lds, (a.ntiles + T / 64 - 1) / (T / 64));
-      *grid_out = grid;
-      hipLaunchKernelGGL(k2, dim3((unsigned)grid), dim3(T), lds, s, a);
-      return;
-    }
-  }
   // the packed-program fast path exists for d = 1 chains of <= 16 flows
   auto kfn = (DM == 1 && kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
                  ? chain_persistent_kernel<DM, kFast, NV, POST, DM == 1 && kFast>

@@ -81,7 +81,6 @@ for s in $STEPS; do
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
-    pf2) run pf2 300 python tools/microbench.py pf2 ;;
     *) echo "unknown step $s" ;;
   esac
 done

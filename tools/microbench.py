@@ -168,20 +168,9 @@ def main():
              {"name": "precise", "env": {}, "math": "precise"}]
         run("C3", v)
         return
-    if which[0] == "pf2":  # prefetch depth study (C2)
-        v = [{"name": "depth1", "env": {}},
-             {"name": "depth2", "env": {"NFN_PREFETCH2": 1}},
-             {"name": "depth2_ablate", "env": {"NFN_PREFETCH2": 1, "NFN_ABLATE_FLOWS": 1}},
-             {"name": "depth1_ablate", "env": {"NFN_ABLATE_FLOWS": 1}},
-             {"name": "depth2_wg2", "env": {"NFN_PREFETCH2": 1, "NFN_WG_PER_CU": 2}},
-             {"name": "depth2_wg4", "env": {"NFN_PREFETCH2": 1, "NFN_WG_PER_CU": 4}}]
-        run("C2", v)
-        return
     if which[0] == "prio":  # wave priority around the tile hand-off
-        v = [{"name": "prio", "env": {"NFN_PRIO": 1}}, {"name": "static", "env": {"NFN_PRIO": 2}},
-             {"name": "noprio", "env": {"NFN_PRIO": 0}},
-             {"name": "prio_b", "env": {"NFN_PRIO": 1}}, {"name": "static_b", "env": {"NFN_PRIO": 2}},
-             {"name": "noprio_b", "env": {"NFN_PRIO": 0}}]
+        v = [{"name": "prio", "env": {"NFN_PRIO": 1}}, {"name": "noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "prio_b", "env": {"NFN_PRIO": 1}}, {"name": "noprio_b", "env": {"NFN_PRIO": 0}}]
         for cfg in ("C2", "C5"):
             run(cfg, v, reps=30, rounds=4)
         return
