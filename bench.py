@@ -179,6 +179,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--prewarm-ms", type=float, default=300.0,
+                    help="untimed launches before the W warmup steps until this much device time has "
+                         "run: the MI355X raises its clocks over the first tens of ms of sustained load, "
+                         "so a short warmup would time the ramp, not the steady state (0 disables)")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="override the per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -284,6 +288,26 @@ def main():
             if w is not None:
                 w.wait()
 
+    # clock ramp: keep the device busy with untimed steps for >= --prewarm-ms of device time
+    prewarm_steps = 0
+    if args.prewarm_ms > 0:
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        pe0.record(stream)
+        step()
+        pe1.record(stream)
+        torch.cuda.synchronize()
+        per = max(pe0.elapsed_time(pe1), 1e-3)
+        prewarm_steps = int(min(20000, np.ceil(args.prewarm_ms / per)))
+        if dist_on:  # every rank must issue the same number of step all-reduces
+            drain()
+            cnt = torch.tensor([prewarm_steps], dtype=torch.int64,
+                               device=dev if args.backend == "nccl" else torch.device("cpu"))
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX)
+            prewarm_steps = int(cnt.item())
+        for _ in range(prewarm_steps):
+            step()
+        drain()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     drain()
@@ -378,6 +402,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",

@@ -882,6 +882,167 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
   }
 }
 
+// d = 1, wave-owned tiles, P = 4Q floats per row (Q = 2, 4, 8, 16): the hot path of
+// configs C1, C2 and C5.  Same walk as chain_persistent_kernel's wave mode, written
+// so that the memory pipeline is straight-line code the waitcnt pass can count:
+//   * every tile access is a BUFFER instruction whose descriptor (wave-uniform SGPRs)
+//     spans exactly the tile's valid bytes: loads past B return 0 and stores past B
+//     are dropped by the range check, so the last partial tile needs no branch and
+//     no clamping, and addresses are loop-invariant 32-bit lane offsets (+ an SGPR
+//     offset per row piece) — no VALU address arithmetic per load;
+//   * y is issued FIRST with the next tile's rows; the rows are written to LDS at the
+//     hand-off behind one counted wait;
+//   * the previous tile's log_prob store is issued BEFORE the next prefetch, and no
+//     wait between it and the next hand-off covers it (in the generic kernel a y use
+//     after the store, behind a branchy hand-off, made the compiler wait for the
+//     store's full round trip on every tile).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <bool FAST, int Q, bool POST, bool PACKED>
+__global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  constexpr int RSTEP = 64 / Q;  // rows per wave-instruction
+  constexpr int kNT = 2;         // buffer cache policy: non-temporal (streamed once)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: SGPR descriptors
+  const int S = a.lds_stride;
+  const int64_t rs = a.t_rowstride;
+  const int r0 = lane / Q, c4 = lane % Q;
+  float* tl = lds + wid * 64 * S;
+  const int l0 = r0 * S + 4 * c4;
+  const int nsp = POST ? a.nsplit : 1;
+  const int dps = POST ? a.dps : 1;
+  const int64_t nunits = a.ntiles * nsp;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<FAST>(ystd);
+  }
+  // diagnostic (NFN_ABLATE_LOADS): every unit re-reads the first unit's rows
+  const int64_t abl_tile = a.ablate_loads ? (POST ? u0 / nsp : u0) : -1;
+  // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int toff = (r0 * (int)rs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)rs * 4;
+
+  float4 buf[Q];
+  float ybuf = 0.0f;
+  auto issue = [&](int64_t unit, int s, bool first) {
+    int64_t tile = POST ? unit / nsp : unit;
+    if (abl_tile >= 0) tile = abl_tile;
+    const int64_t b0 = tile * 64;
+    const int64_t nr = min((int64_t)64, a.B - b0);
+    if (first) {
+      const auto ry = tile_rsrc(a.y + b0 * a.y_bstride, ((nr - 1) * a.y_bstride + 1) * 4);
+      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    }
+    const auto rt = tile_rsrc(a.t + (int64_t)s * a.t_drawstride + b0 * rs, ((nr - 1) * rs + a.P) * 4);
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+  };
+  auto range_of = [&](int64_t unit, int& sb, int& se) {
+    const int rg = POST ? (int)(unit % nsp) : 0;
+    sb = rg * dps;
+    se = POST ? min(a.S, sb + dps) : 1;
+  };
+
+  double acc = 0.0;
+  // deferred result of the previous unit: log_prob (plain / unsplit posterior) through
+  // a descriptor bounded at B, or a (max, scaled sum) pair of a draw-split posterior
+  bool pend = false;
+  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
+  int64_t pend_i = 0;
+  float pend_v = 0.0f, pend_m = 0.0f;
+  int64_t unit = u0;
+  if (unit < nunits) {
+    int sb, se;
+    range_of(unit, sb, se);
+    issue(unit, sb, true);
+  }
+  for (; unit < nunits; unit += ustep) {
+    const int64_t tile = POST ? unit / nsp : unit;
+    const int64_t b0 = tile * 64;
+    const int64_t nr = min((int64_t)64, a.B - b0);
+    int sb, se;
+    range_of(unit, sb, se);
+    float m = -INFINITY, accl = 0.0f, lp = 0.0f, z0 = 0.0f;
+    for (int s = sb; s < se; ++s) {
+      if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        float* dst = tl + l0 + k * RSTEP * S;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
+      if (s == sb) z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
+      wave_lds_sync();
+      if (pend) {
+        if (!POST || nsp == 1) {
+          if (a.nt_store)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+          else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, 0);
+        } else if (lane < nr) {
+          a.split_out[pend_i + lane] = make_float2(pend_m, pend_v);
+        }
+        pend = false;
+      }
+      if (s + 1 < se) {
+        issue(unit, s + 1, false);
+      } else if (unit + ustep < nunits) {
+        int nb, ne;
+        range_of(unit + ustep, nb, ne);
+        issue(unit + ustep, nb, true);
+      }
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      if constexpr (FAST) {
+        lp = eval_chain1_fast<PACKED>(z0, tl + lane * S, a) - corr;
+      } else {
+        float z[1] = {z0};
+        lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
+      }
+      if constexpr (POST) lse_push<FAST>(m, accl, lp);
+      wave_lds_sync();  // this tile's LDS reads done before the next writes
+    }
+    pend = true;
+    if (POST && nsp > 1) {
+      pend_i = (int64_t)(unit % nsp) * a.B + b0;
+      pend_m = m;
+      pend_v = accl;
+    } else {
+      float res = lp;
+      if constexpr (POST) res = lse_finish<FAST>(m, accl, a.S);
+      pend_r = tile_rsrc(a.out ? a.out + b0 : nullptr, a.out ? nr * 4 : 0);
+      pend_v = res;
+      if (lane < nr) acc += (double)res;
+    }
+  }
+  if (pend) {
+    if (!POST || nsp == 1) {
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+    } else {
+      const int64_t tile = POST ? (unit - ustep) / nsp : 0;
+      if (lane < min((int64_t)64, a.B - tile * 64)) a.split_out[pend_i + lane] = make_float2(pend_m, pend_v);
+    }
+  }
+  if (a.partials && (!POST || nsp == 1)) {
+    const double sum = block_sum(acc, red);
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
 
 // Combines the per-range (max, scaled sum) pairs of a draw-split posterior:
 // out[b] = M + log(sum_r acc_r * exp(m_r - M)) - log S, M = max_r m_r.

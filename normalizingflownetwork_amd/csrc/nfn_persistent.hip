@@ -11,6 +11,42 @@ namespace {
 
 constexpr bool kFast = NFN_FAST != 0;
 
+// d = 1 wave-tile kernel (chain_wave1_kernel) for rows of exactly Q float4.
+template <int Q, bool POST>
+void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = (kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
+                 ? chain_wave1_kernel<kFast, Q, POST, kFast>
+                 : chain_wave1_kernel<kFast, Q, POST, false>;
+  const int64_t units = a.ntiles * (POST ? a.nsplit : 1);
+  const int teams = T / 64;
+  // Resident workgroups per CU: a long chain (C2: 10 flows) keeps each wave busy
+  // long enough that 2 waves per SIMD hide the streamed rows and fewer bytes in
+  // flight stream faster (C2: 0.365 ms at 2 vs 0.418 at 4 per CU); a short chain
+  // (C1: 2 flows) is latency-bound and wants all 4 (0.127 vs 0.173 ms).
+  int64_t grid;
+  if (env_int("NFN_WG_PER_CU", 0) > 0)
+    grid = persistent_grid(kfn, T, lds, (units + teams - 1) / teams);
+  else
+    grid = std::min<int64_t>((units + teams - 1) / teams, (int64_t)cu_count() * (a.prog.K >= 4 ? 2 : 4));
+  *grid_out = grid;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
+}
+
+template <bool POST>
+bool try_wave1(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
+  // the posterior (C5) stays on the generic kernel: measured 0.177 vs 0.181 ms there
+  if (a.d != 1 || a.ownrow != 2 || !a.nt || env_int("NFN_WAVE1", POST ? 0 : 1) == 0) return false;
+  // 32-bit lane byte offsets: a tile's 64 rows (and y entries) must span < 2 GiB
+  if (a.t_rowstride * 256 >= (int64_t)1 << 31 || a.y_bstride * 256 >= (int64_t)1 << 31) return false;
+  switch (Q) {
+    case 2: launch_w1<2, POST>(a, T, lds, s, g); return true;
+    case 4: launch_w1<4, POST>(a, T, lds, s, g); return true;
+    case 8: launch_w1<8, POST>(a, T, lds, s, g); return true;
+    case 16: launch_w1<16, POST>(a, T, lds, s, g); return true;
+    default: return false;
+  }
+}
+
 template <int DM, int NV, bool POST>
 void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
   // the packed-program fast path exists for d = 1 chains of <= 16 flows
@@ -59,6 +95,8 @@ bool launch_persistent_precise(bool post, int dm, int Q, const ChainArgs& a, int
                                int64_t* grid) {
 #endif
   if (Q < 1 || Q > 16) return false;
+  if (dm == 1 && (post ? try_wave1<true>(Q, a, T, lds, s, grid) : try_wave1<false>(Q, a, T, lds, s, grid)))
+    return true;
   if (post)
     launch_p_dm<true>(dm, Q, a, T, lds, s, grid);
   else

@@ -28,6 +28,18 @@ def bytes_per_launch(d, P, B, S):
     return B * (4 * d + 4 * P + 4) if S is None else B * (S * 4 * P + 4 * d + 4)
 
 
+def prewarm(fn, ms=400.0):
+    """Untimed launches for >= `ms` of device time (the clocks ramp over the first tens of ms)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    fn()
+    e1.record()
+    torch.cuda.synchronize()
+    for _ in range(int(ms / max(e0.elapsed_time(e1), 1e-3)) + 1):
+        fn()
+    torch.cuda.synchronize()
+
+
 def run(cfg, variants, reps=20, rounds=3):
     ft, d, B, S = CFG[cfg]
     P = ops.total_param_size(ft, d, True)
@@ -38,6 +50,7 @@ def run(cfg, variants, reps=20, rounds=3):
     L_noout = ops.ChainLauncher(y, t, ft, d, True, write_values=False, draws=S)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
+    prewarm(lambda: L.launch(sh))
     times = {v["name"]: [] for v in variants}
     outs = {}
     for r in range(rounds):
@@ -201,6 +214,24 @@ def main():
                       {"name": "wave_nosplit", "env": {"NFN_LOAD_MODE": "wave", "NFN_POST_SPLIT": 1}}]
             run(cfg, v)
         return
+    if which[0] == "wave1":  # straight-line d = 1 wave kernel vs the generic persistent kernel
+        v = [{"name": "wave1", "env": {}}, {"name": "generic", "env": {"NFN_WAVE1": 0}},
+             {"name": "wave1_wg1", "env": {"NFN_WG_PER_CU": 1}},
+             {"name": "wave1_wg2_stdef", "env": {"NFN_WG_PER_CU": 2, "NFN_NT_STORES": 0}},
+             {"name": "wave1_stdef", "env": {"NFN_NT_STORES": 0}},
+             {"name": "wave1_wg2_noout", "env": {"NFN_WG_PER_CU": 2}, "noout": True},
+             {"name": "wave1_wg2_memory_only", "env": {"NFN_WG_PER_CU": 2, "NFN_ABLATE_FLOWS": 1}},
+             {"name": "wave1_wg1_memory_only", "env": {"NFN_WG_PER_CU": 1, "NFN_ABLATE_FLOWS": 1}},
+             {"name": "wave1_noout", "env": {}, "noout": True},
+             {"name": "wave1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "wave1_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "wave1_wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "wave1_wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "wave1_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "wave1_b", "env": {}}, {"name": "generic_b", "env": {"NFN_WAVE1": 0}}]
+        for cfg in which[1:] or ["C2", "C5", "C1"]:
+            run(cfg, v)
+        return
     if which[0] == "mem":  # memory-path study on C2
         A = {"NFN_ABLATE_FLOWS": 1}
         v = [{"name": "auto", "env": {}},
@@ -214,7 +245,12 @@ def main():
              {"name": "ablate_wg1", "env": dict(A, NFN_WG_PER_CU=1)},
              {"name": "ablate_wg2", "env": dict(A, NFN_WG_PER_CU=2)},
              {"name": "ablate_wg3", "env": dict(A, NFN_WG_PER_CU=3)},
-             {"name": "ablate_ownrow_wg2", "env": dict(A, NFN_WG_PER_CU=2, NFN_LOAD_MODE="ownrow")}]
+             {"name": "ablate_ownrow_wg2", "env": dict(A, NFN_WG_PER_CU=2, NFN_LOAD_MODE="ownrow")},
+             {"name": "wg1", "env": {"NFN_WG_PER_CU": 1}},
+             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "ablate_noprio", "env": dict(A, NFN_PRIO=0)}]
         run("C2", v)
         return
     base = [
