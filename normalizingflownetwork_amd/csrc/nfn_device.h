@@ -883,27 +883,28 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
 }
 
 // d = 1, wave-owned tiles, P = 4Q floats per row (Q = 2, 4, 8, 16): the hot path of
-// configs C1, C2 and C5.  Same walk as chain_persistent_kernel's wave mode, written
+// configs C1 and C2 (forward; the posterior stays on chain_persistent_kernel).  Same walk as chain_persistent_kernel's wave mode, written
 // so that the memory pipeline is straight-line code the waitcnt pass can count:
 //   * every tile access is a BUFFER instruction whose descriptor (wave-uniform SGPRs)
 //     spans exactly the tile's valid bytes: loads past B return 0 and stores past B
 //     are dropped by the range check, so the last partial tile needs no branch and
 //     no clamping, and addresses are loop-invariant 32-bit lane offsets (+ an SGPR
 //     offset per row piece) — no VALU address arithmetic per load;
-//   * y is issued FIRST with the next tile's rows; the rows are written to LDS at the
-//     hand-off behind one counted wait;
-//   * the previous tile's log_prob store is issued BEFORE the next prefetch, and no
-//     wait between it and the next hand-off covers it (in the generic kernel a y use
-//     after the store, behind a branchy hand-off, made the compiler wait for the
-//     store's full round trip on every tile).
+//   * y is issued FIRST with a tile's rows, one tile ahead; the rows are written to
+//     LDS at the hand-off behind one counted wait;
+//   * log_prob leaves in batches (see `flush`), never waited on by the next hand-off
+//     (in the generic kernel a y use after the store, behind a branchy hand-off, made
+//     the compiler wait for the store's full round trip on every tile).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <bool FAST, int Q, bool POST, bool PACKED>
+template <bool FAST, int Q, int G, bool PACKED>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
+  static_assert(G == 1 || G == 4, "tiles per unit: 1 or 4");
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
+  __shared__ float obuf[G == 4 ? (kMaxBlock / 64) * 256 : 1];  // per wave: a unit's log_prob
   constexpr int RSTEP = 64 / Q;  // rows per wave-instruction
   constexpr int kNT = 2;         // buffer cache policy: non-temporal (streamed once)
   const int tid = threadIdx.x;
@@ -912,10 +913,10 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   const int64_t rs = a.t_rowstride;
   const int r0 = lane / Q, c4 = lane % Q;
   float* tl = lds + wid * 64 * S;
+  float* ob = obuf + (G == 4 ? wid * 256 : 0);
   const int l0 = r0 * S + 4 * c4;
-  const int nsp = POST ? a.nsplit : 1;
-  const int dps = POST ? a.dps : 1;
-  const int64_t nunits = a.ntiles * nsp;
+  const int64_t ntiles = a.ntiles;
+  const int64_t nunits = (ntiles + G - 1) / G;  // a unit = G consecutive 64-row tiles
   const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
   const bool norm = a.y_mean != nullptr;
@@ -925,56 +926,52 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     ystd = a.y_std[0];
     corr = f_log<FAST>(ystd);
   }
-  // diagnostic (NFN_ABLATE_LOADS): every unit re-reads the first unit's rows
-  const int64_t abl_tile = a.ablate_loads ? (POST ? u0 / nsp : u0) : -1;
+  // diagnostic (NFN_ABLATE_LOADS): every tile re-reads the wave's first tile
+  const int64_t abl_tile = a.ablate_loads ? u0 * G : -1;
   // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
   const int yoff = lane * (int)a.y_bstride * 4;
   const int toff = (r0 * (int)rs + 4 * c4) * 4;
   const int kstep = RSTEP * (int)rs * 4;
 
+  // Tiles past the end are issued too, through empty descriptors (no memory traffic,
+  // zeros returned): every path then holds the same loads in the same order and the
+  // waitcnt pass counts each hand-off's wait exactly.
   float4 buf[Q];
-  float ybuf = 0.0f;
-  auto issue = [&](int64_t unit, int s, bool first) {
-    int64_t tile = POST ? unit / nsp : unit;
+  float ybuf;
+  auto issue = [&](int64_t tile) {
     if (abl_tile >= 0) tile = abl_tile;
     const int64_t b0 = tile * 64;
-    const int64_t nr = min((int64_t)64, a.B - b0);
-    if (first) {
-      const auto ry = tile_rsrc(a.y + b0 * a.y_bstride, ((nr - 1) * a.y_bstride + 1) * 4);
-      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
-    }
-    const auto rt = tile_rsrc(a.t + (int64_t)s * a.t_drawstride + b0 * rs, ((nr - 1) * rs + a.P) * 4);
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const auto rt = tile_rsrc(a.t + b0c * rs, nr > 0 ? ((nr - 1) * rs + a.P) * 4 : 0);
 #pragma unroll
     for (int k = 0; k < Q; ++k)
       buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
   };
-  auto range_of = [&](int64_t unit, int& sb, int& se) {
-    const int rg = POST ? (int)(unit % nsp) : 0;
-    sb = rg * dps;
-    se = POST ? min(a.S, sb + dps) : 1;
-  };
 
   double acc = 0.0;
-  // deferred result of the previous unit: log_prob (plain / unsplit posterior) through
-  // a descriptor bounded at B, or a (max, scaled sum) pair of a draw-split posterior
-  bool pend = false;
+  // The previous unit's log_prob, stored through a descriptor bounded at B (empty
+  // before the first unit: the store is always issued).  It is issued right AFTER
+  // the next prefetch, so the next hand-off's wait does not cover it; with G = 4 a
+  // unit's 256 values leave as one contiguous 1 KiB store (float4 per lane) per 4
+  // tiles instead of four 256-byte stores.
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
-  int64_t pend_i = 0;
-  float pend_v = 0.0f, pend_m = 0.0f;
-  int64_t unit = u0;
-  if (unit < nunits) {
-    int sb, se;
-    range_of(unit, sb, se);
-    issue(unit, sb, true);
-  }
-  for (; unit < nunits; unit += ustep) {
-    const int64_t tile = POST ? unit / nsp : unit;
-    const int64_t b0 = tile * 64;
-    const int64_t nr = min((int64_t)64, a.B - b0);
-    int sb, se;
-    range_of(unit, sb, se);
-    float m = -INFINITY, accl = 0.0f, lp = 0.0f, z0 = 0.0f;
-    for (int s = sb; s < se; ++s) {
+  float4 pend_v = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto flush = [&]() {
+    if constexpr (G == 4)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, pend_v), pend_r, lane * 16, 0, kNT);
+    else
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v.x), pend_r, lane * 4, 0, kNT);
+  };
+  issue(u0 * G);
+  for (int64_t unit = u0; unit < nunits; unit += ustep) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t tile = unit * G + g;  // may be past the end in the last unit (empty)
+      const int64_t b0 = tile * 64;
+      const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
       if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
 #pragma unroll
       for (int k = 0; k < Q; ++k) {
@@ -984,58 +981,36 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
         dst[2] = buf[k].z;
         dst[3] = buf[k].w;
       }
-      if (s == sb) z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
+      const float z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
       wave_lds_sync();
-      if (pend) {
-        if (!POST || nsp == 1) {
-          if (a.nt_store)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
-          else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, 0);
-        } else if (lane < nr) {
-          a.split_out[pend_i + lane] = make_float2(pend_m, pend_v);
-        }
-        pend = false;
-      }
-      if (s + 1 < se) {
-        issue(unit, s + 1, false);
-      } else if (unit + ustep < nunits) {
-        int nb, ne;
-        range_of(unit + ustep, nb, ne);
-        issue(unit + ustep, nb, true);
-      }
+      issue(g + 1 < G ? tile + 1 : (unit + ustep) * G);
+      if (g == 0) flush();
       if (a.prio) __builtin_amdgcn_s_setprio(0);
+      float lp;
       if constexpr (FAST) {
         lp = eval_chain1_fast<PACKED>(z0, tl + lane * S, a) - corr;
       } else {
         float z[1] = {z0};
         lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
       }
-      if constexpr (POST) lse_push<FAST>(m, accl, lp);
+      if (lane < nr) acc += (double)lp;
+      if constexpr (G == 4) {
+        ob[g * 64 + lane] = lp;
+      } else {
+        pend_v.x = lp;
+        pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+      }
       wave_lds_sync();  // this tile's LDS reads done before the next writes
     }
-    pend = true;
-    if (POST && nsp > 1) {
-      pend_i = (int64_t)(unit % nsp) * a.B + b0;
-      pend_m = m;
-      pend_v = accl;
-    } else {
-      float res = lp;
-      if constexpr (POST) res = lse_finish<FAST>(m, accl, a.S);
-      pend_r = tile_rsrc(a.out ? a.out + b0 : nullptr, a.out ? nr * 4 : 0);
-      pend_v = res;
-      if (lane < nr) acc += (double)res;
+    if constexpr (G == 4) {
+      pend_v = *reinterpret_cast<const float4*>(ob + 4 * lane);
+      const int64_t ub = unit * 256;
+      const int64_t nu = max((int64_t)0, min((int64_t)256, a.B - ub));
+      pend_r = tile_rsrc(a.out && nu > 0 ? a.out + ub : a.out, a.out ? nu * 4 : 0);
     }
   }
-  if (pend) {
-    if (!POST || nsp == 1) {
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
-    } else {
-      const int64_t tile = POST ? (unit - ustep) / nsp : 0;
-      if (lane < min((int64_t)64, a.B - tile * 64)) a.split_out[pend_i + lane] = make_float2(pend_m, pend_v);
-    }
-  }
-  if (a.partials && (!POST || nsp == 1)) {
+  flush();
+  if (a.partials) {
     const double sum = block_sum(acc, red);
     if (tid == 0) {
       a.partials[blockIdx.x] = sum;

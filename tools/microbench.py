@@ -214,22 +214,19 @@ def main():
                       {"name": "wave_nosplit", "env": {"NFN_LOAD_MODE": "wave", "NFN_POST_SPLIT": 1}}]
             run(cfg, v)
         return
-    if which[0] == "wave1":  # straight-line d = 1 wave kernel vs the generic persistent kernel
-        v = [{"name": "wave1", "env": {}}, {"name": "generic", "env": {"NFN_WAVE1": 0}},
-             {"name": "wave1_wg1", "env": {"NFN_WG_PER_CU": 1}},
-             {"name": "wave1_wg2_stdef", "env": {"NFN_WG_PER_CU": 2, "NFN_NT_STORES": 0}},
-             {"name": "wave1_stdef", "env": {"NFN_NT_STORES": 0}},
-             {"name": "wave1_wg2_noout", "env": {"NFN_WG_PER_CU": 2}, "noout": True},
-             {"name": "wave1_wg2_memory_only", "env": {"NFN_WG_PER_CU": 2, "NFN_ABLATE_FLOWS": 1}},
-             {"name": "wave1_wg1_memory_only", "env": {"NFN_WG_PER_CU": 1, "NFN_ABLATE_FLOWS": 1}},
-             {"name": "wave1_noout", "env": {}, "noout": True},
-             {"name": "wave1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
-             {"name": "wave1_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
-             {"name": "wave1_wg2", "env": {"NFN_WG_PER_CU": 2}},
-             {"name": "wave1_wg3", "env": {"NFN_WG_PER_CU": 3}},
-             {"name": "wave1_noprio", "env": {"NFN_PRIO": 0}},
-             {"name": "wave1_b", "env": {}}, {"name": "generic_b", "env": {"NFN_WAVE1": 0}}]
-        for cfg in which[1:] or ["C2", "C5", "C1"]:
+    if which[0] == "wave1":  # straight-line d = 1 wave kernel: unit size x occupancy
+        v = [{"name": "g4", "env": {}}, {"name": "generic", "env": {"NFN_WAVE1": 0}},
+             {"name": "g1", "env": {"NFN_UNIT_TILES": 1}},
+             {"name": "g4_wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "g4_wg4", "env": {"NFN_WG_PER_CU": 4}},
+             {"name": "g4_wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "g4_noout", "env": {}, "noout": True},
+             {"name": "g1_noout", "env": {"NFN_UNIT_TILES": 1}, "noout": True},
+             {"name": "g4_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "g4_memory_only", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": 2}},
+             {"name": "g4_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "g4_b", "env": {}}, {"name": "g1_b", "env": {"NFN_UNIT_TILES": 1}}]
+        for cfg in which[1:] or ["C2", "C1"]:
             run(cfg, v)
         return
     if which[0] == "mem":  # memory-path study on C2

@@ -1,18 +1,20 @@
-// stream_ceiling.hip — HBM read-stream ceilings on MI355X for the chain kernels'
-// access pattern: persistent waves, each owning 8 KiB tiles (64 rows x 128 B) of
-// one large buffer, the next tile prefetched while the current one is "used".
-//   mode 0: global_load_dwordx4 into registers, default cache policy
-//   mode 1: the same, non-temporal
-//   mode 2: global_load_lds_dwordx4 (LDS-DMA) into a per-wave LDS slot, nt
-//   mode 3: LDS-DMA, default policy
+// stream_ceiling.hip — HBM stream ceilings on MI355X for the chain kernels' access
+// pattern: persistent waves, each owning 8 KiB tiles (64 rows x 128 B) of one large
+// buffer, the next tile prefetched into registers while the current one is "used".
+// Axes (one line per combination):
+//   extra : 0 = t rows only, 1 = + a 256 B y load per tile, 2 = + y + a 256 B log_prob
+//           store per tile (nt), 3 = as 2 with a default-policy store
+//   work  : a dependent chain of `work` v_fma per tile after the hand-off (emulates
+//           the flow math; ~300 VALU per sample is the C2 chain)
+//   wg/CU : resident 4-wave workgroups per CU
 // Build: hipcc --offload-arch=gfx950 -O3 tools/stream_ceiling.hip -o tools/stream_ceiling
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
 #include <stdlib.h>
 
-#include <vector>
 #include <algorithm>
+#include <vector>
 
 #define CHECK(x)                                                              \
   do {                                                                        \
@@ -25,65 +27,102 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int MODE, int NV>
-__global__ void __launch_bounds__(256) stream_kernel(const float* __restrict__ src, int64_t ntiles,
-                                                     float* __restrict__ sink) {
-  __shared__ f32x4 slot[4][2][512];  // per wave: two 8 KiB slots
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t w0 = (int64_t)blockIdx.x * 4 + wid, ws = (int64_t)gridDim.x * 4;
-  f32x4 acc = {0, 0, 0, 0};
-  if constexpr (MODE <= 1) {
-    f32x4 buf[NV];
-    int64_t t = w0;
-    auto issue = [&](int64_t tile) {
-      const f32x4* p = reinterpret_cast<const f32x4*>(src + tile * 2048) + lane;
-#pragma unroll
-      for (int k = 0; k < NV; ++k) buf[k] = MODE == 1 ? __builtin_nontemporal_load(p + k * 64) : p[k * 64];
-    };
-    if (t < ntiles) issue(t);
-    for (; t < ntiles; t += ws) {
-      f32x4 cur[NV];
-#pragma unroll
-      for (int k = 0; k < NV; ++k) cur[k] = buf[k];
-      if (t + ws < ntiles) issue(t + ws);
-#pragma unroll
-      for (int k = 0; k < NV; ++k) acc += cur[k];
-    }
-  } else {
-    int64_t t = w0;
-    int sl = 0;
-    auto issue = [&](int64_t tile, int s) {
-      const float* p = src + tile * 2048 + lane * 4;
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        __builtin_amdgcn_global_load_lds(p + k * 256, (__attribute__((address_space(3))) void*)&slot[wid][s][k * 64],
-                                         16, 0, MODE == 2 ? 2 : 0);
-    };
-    if (t < ntiles) issue(t, 0);
-    for (; t < ntiles; t += ws) {
-      if (t + ws < ntiles) {
-        issue(t + ws, sl ^ 1);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_wave_barrier();
-      acc += slot[wid][sl][lane * 8];
-      sl ^= 1;
-    }
-  }
-  if (acc.x == 123.456f) sink[threadIdx.x] = acc.y + acc.z + acc.w;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
 }
 
-template <int MODE>
-float run(const float* d, int64_t ntiles, float* sink, int grid, int reps) {
+template <int EXTRA>
+__global__ void __launch_bounds__(256) stream_kernel(const float* __restrict__ t, const float* __restrict__ y,
+                                                     float* __restrict__ out, int64_t ntiles, int work,
+                                                     float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * 4 + wid, ws = (int64_t)gridDim.x * 4;
+  f32x4 buf[8];
+  float yb = 0.f, acc = 0.f;
+  auto issue = [&](int64_t tile) {
+    const int64_t tc = tile < ntiles ? tile : 0;
+    const int nb = tile < ntiles ? 8192 : 0;
+    if (EXTRA >= 1)
+      yb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(y + tc * 64, nb ? 256 : 0), lane * 4, 0, 0));
+    const auto r = rsrc(t + tc * 2048, nb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, k * 1024, 2));
+  };
+  issue(w0);
+  float pv = 0.f;
+  auto pr = rsrc(out, 0);
+  for (int64_t tile = w0; tile < ntiles; tile += ws) {
+    f32x4 s = buf[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) s += buf[k];
+    float v = s.x + s.y + s.z + s.w + yb;
+    if (EXTRA >= 2) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pv), pr, lane * 4, 0, EXTRA == 2 ? 2 : 0);
+    issue(tile + ws);
+    for (int i = 0; i < work; ++i) v = fmaf(v, 0.999f, 0.5f);
+    acc += v;
+    pv = v;
+    pr = rsrc(out + tile * 64, 256);
+  }
+  if (EXTRA >= 2) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pv), pr, lane * 4, 0, 2);
+  if (acc == 123.456f) sink[threadIdx.x] = acc;
+}
+
+// G consecutive tiles per wave step; the step's G x 256 B of log_prob leave as
+// G/4 contiguous 1 KiB stores (float4 per lane) after the step's last tile.
+template <int G>
+__global__ void __launch_bounds__(256) stream_group_kernel(const float* __restrict__ t, const float* __restrict__ y,
+                                                           float* __restrict__ out, int64_t ntiles,
+                                                           float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * 4 + wid, ws = (int64_t)gridDim.x * 4;
+  const int64_t nunits = ntiles / G;
+  f32x4 buf[8];
+  float yb = 0.f, acc = 0.f;
+  auto issue = [&](int64_t tile) {
+    const int64_t tc = tile < ntiles ? tile : 0;
+    const int nb = tile < ntiles ? 8192 : 0;
+    yb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(y + tc * 64, nb ? 256 : 0), lane * 4, 0, 0));
+    const auto r = rsrc(t + tc * 2048, nb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, k * 1024, 2));
+  };
+  issue(w0 * G);
+  f32x4 pv[G / 4];
+  auto pr = rsrc(out, 0);
+  for (int64_t u = w0; u < nunits; u += ws) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      f32x4 s = buf[0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) s += buf[k];
+      const float v = s.x + s.y + s.z + s.w + yb;
+      issue(g + 1 < G ? u * G + g + 1 : (u + ws) * G);
+      if (g == 0) {
+#pragma unroll
+        for (int i = 0; i < G / 4; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(pv[i], pr, lane * 16, i * 1024, 2);
+      }
+      acc += v;
+      pv[g / 4][g % 4] = v;
+    }
+    pr = rsrc(out + u * G * 64, G * 256);
+  }
+#pragma unroll
+  for (int i = 0; i < G / 4; ++i) __builtin_amdgcn_raw_buffer_store_b128(pv[i], pr, lane * 16, i * 1024, 2);
+  if (acc == 123.456f) sink[threadIdx.x] = acc;
+}
+
+template <int G>
+float run_group(const float* t, const float* y, float* out, int64_t ntiles, float* sink, int grid, int reps) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   std::vector<float> ts;
   for (int r = 0; r < reps; ++r) {
     CHECK(hipEventRecord(e0));
-    hipLaunchKernelGGL((stream_kernel<MODE, 8>), dim3(grid), dim3(256), 0, 0, d, ntiles, sink);
+    hipLaunchKernelGGL(stream_group_kernel<G>, dim3(grid), dim3(256), 0, 0, t, y, out, ntiles, sink);
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     float ms;
@@ -91,32 +130,73 @@ float run(const float* d, int64_t ntiles, float* sink, int grid, int reps) {
     ts.push_back(ms);
   }
   std::sort(ts.begin(), ts.end());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return ts[ts.size() / 2];
+}
+
+template <int EXTRA>
+float run(const float* t, const float* y, float* out, int64_t ntiles, int work, float* sink, int grid, int reps) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < reps; ++r) {
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(stream_kernel<EXTRA>, dim3(grid), dim3(256), 0, 0, t, y, out, ntiles, work, sink);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
   return ts[ts.size() / 2];
 }
 
 int main() {
   const int64_t B = 1 << 24, P = 32;
-  const int64_t bytes = B * P * 4;
+  const int64_t tbytes = B * P * 4;
   const int64_t ntiles = B / 64;
-  float *d, *sink;
-  CHECK(hipMalloc(&d, bytes));
+  float *t, *y, *out, *sink;
+  CHECK(hipMalloc(&t, tbytes));
+  CHECK(hipMalloc(&y, B * 4));
+  CHECK(hipMalloc(&out, B * 4));
   CHECK(hipMalloc(&sink, 4096));
-  CHECK(hipMemset(d, 0, bytes));
+  CHECK(hipMemset(t, 0, tbytes));
+  CHECK(hipMemset(y, 0, B * 4));
   int cus = 256;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  // warm the clocks: ~400 ms of streaming
-  for (int i = 0; i < 1000; ++i)
-    hipLaunchKernelGGL((stream_kernel<1, 8>), dim3(cus * 4), dim3(256), 0, 0, d, ntiles, sink);
+  for (int i = 0; i < 1000; ++i)  // ~0.4 s: let the clocks ramp
+    hipLaunchKernelGGL(stream_kernel<0>, dim3(cus * 2), dim3(256), 0, 0, t, y, out, ntiles, 0, sink);
   CHECK(hipDeviceSynchronize());
-  for (int wpc : {1, 2, 3, 4}) {
+  const double bytes[4] = {(double)tbytes, (double)tbytes + 4.0 * B, (double)tbytes + 8.0 * B, (double)tbytes + 8.0 * B};
+  for (int wpc : {1, 2, 4}) {
     const int grid = cus * wpc;
-    float m0 = run<0>(d, ntiles, sink, grid, 30);
-    float m1 = run<1>(d, ntiles, sink, grid, 30);
-    float m2 = run<2>(d, ntiles, sink, grid, 30);
-    float m3 = run<3>(d, ntiles, sink, grid, 30);
-    printf("wg/CU=%d  regs-default %.4f ms %.0f GB/s | regs-nt %.4f ms %.0f GB/s | lds-dma-nt %.4f ms %.0f GB/s | "
-           "lds-dma-default %.4f ms %.0f GB/s\n",
-           wpc, m0, bytes / m0 / 1e6, m1, bytes / m1 / 1e6, m2, bytes / m2 / 1e6, m3, bytes / m3 / 1e6);
+    const double b = (double)tbytes + 8.0 * B;
+    const float g4 = run_group<4>(t, y, out, ntiles, sink, grid, 20);
+    const float g16 = run_group<16>(t, y, out, ntiles, sink, grid, 20);
+    const float g32 = run_group<32>(t, y, out, ntiles, sink, grid, 20);
+    printf("grouped stores wg/CU=%d | 1KiB/4 tiles %.4f ms %.0f GB/s | 4KiB/16 tiles %.4f ms %.0f GB/s | "
+           "8KiB/32 tiles %.4f ms %.0f GB/s\n", wpc, g4, b / g4 / 1e6, g16, b / g16 / 1e6, g32, b / g32 / 1e6);
+    fflush(stdout);
+  }
+  for (int work : {0, 40}) {
+    for (int wpc : {1, 2, 3, 4}) {
+      const int grid = cus * wpc;
+      float m[4];
+      m[0] = run<0>(t, y, out, ntiles, work, sink, grid, 20);
+      m[1] = run<1>(t, y, out, ntiles, work, sink, grid, 20);
+      m[2] = run<2>(t, y, out, ntiles, work, sink, grid, 20);
+      m[3] = run<3>(t, y, out, ntiles, work, sink, grid, 20);
+      printf("work=%4d wg/CU=%d |", work, wpc);
+      const char* nm[4] = {"t", "t+y", "t+y+out(nt)", "t+y+out(def)"};
+      for (int e = 0; e < 4; ++e) printf(" %s %.4f ms %.0f GB/s |", nm[e], m[e], bytes[e] / m[e] / 1e6);
+      printf("\n");
+      fflush(stdout);
+    }
   }
   return 0;
 }
