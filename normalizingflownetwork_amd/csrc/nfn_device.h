@@ -966,6 +966,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v.x), pend_r, lane * 4, 0, kNT);
   };
   issue(u0 * G);
+  flush();  // empty: every path into the loop ends [loads][store] (counted waits)
   for (int64_t unit = u0; unit < nunits; unit += ustep) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -1370,6 +1371,109 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     }
   }
   if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
+  if (a.partials) {
+    const double sum = block_sum(acc, red);
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
+
+// chain_group_kernel's walk for contiguous parameter rows (row stride == P), with the
+// memory pipeline of chain_wave1_kernel: a wave tile of R = 64 / G rows is one
+// contiguous block streamed by buffer loads at lane-linear offsets through a
+// descriptor bounded at B (zeros past the end, empty descriptors past the last
+// tile), y and log_prob by buffer instructions too, and no branch between a load
+// and its use: lanes whose slot lies past the tile write their float4 to the pad
+// after the last wave slot.  Plain chain only (the posterior keeps chain_group_kernel).
+template <int G, int DPL, bool FAST, int NV>
+__global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  constexpr int R = 64 / G;  // samples per wave tile
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sl = lane / G;
+  const int j = lane - sl * G;
+  const int Q = a.P >> 2;
+  const int S = a.lds_stride;
+  const int nslots = R * Q;  // float4 pieces per tile
+  float* tl = lds + wid * R * S;
+  float* pad = lds + (kMaxBlock / 64) * R * S;  // scratch for out-of-tile slots
+  int loff[NV];  // LDS float offset of this lane's slot k (tile-invariant)
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = lane + 64 * k;
+    loff[k] = q < nslots ? (int)(tl - lds) + (q / Q) * S + 4 * (q % Q) : (int)(pad - lds);
+  }
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int tbytes = R * a.P * 4;  // one full tile (< 2 GiB: P <= 2^24 / R)
+  const int64_t ybs = a.y_bstride;
+  const int abl = a.ablate_loads;
+  float4 buf[NV];
+  float ybuf[DPL];
+  auto issue = [&](int64_t tile) {
+    if (abl) tile = u0;
+    const int64_t b0 = tile * R;
+    const int64_t nr = max((int64_t)0, min((int64_t)R, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * ybs, nr > 0 ? ((nr - 1) * ybs + a.d) * 4 : 0);
+#pragma unroll
+    for (int i = 0; i < DPL; ++i)
+      ybuf[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             ry, (int)((sl * ybs + j + G * i) * 4), 0, 0));
+    const auto rt = tile_rsrc(a.t + b0c * a.P, (int)(nr * a.P * 4));
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, lane * 16, k * 1024, kNT));
+    (void)tbytes;
+  };
+  float corr = 0.0f;
+  if (a.y_mean) {
+    for (int i = 0; i < a.d; ++i) corr += f_log<FAST>(a.y_std[i]);
+  }
+  float ymean[DPL], yrstd[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) {
+    const int jj = j + G * i;
+    ymean[i] = (a.y_mean && jj < a.d) ? a.y_mean[jj] : 0.0f;
+    yrstd[i] = (a.y_mean && jj < a.d) ? a.y_std[jj] : 1.0f;
+  }
+  const bool norm = a.y_mean != nullptr;
+  double acc = 0.0;
+  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
+  float pend_v = 0.0f;
+  issue(u0);
+  // an (empty) store behind the first prefetch too: every path into the loop then
+  // ends [loads][store] and the hand-off waits with vmcnt(1), not vmcnt(0)
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  for (int64_t tile = u0; tile < a.ntiles; tile += ustep) {
+    const int64_t b0 = tile * R;
+    const int64_t nr = max((int64_t)0, min((int64_t)R, a.B - b0));
+    if (a.prio) __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
+    float z[DPL];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) z[i] = norm ? f_div<FAST>(ybuf[i] - ymean[i], yrstd[i]) : ybuf[i];
+    wave_lds_sync();
+    issue(tile + ustep);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
+    const float lp = eval_chain_gd<G, DPL, FAST>(z, tl + sl * S, a, j) - corr;
+    wave_lds_sync();  // this tile's LDS reads done before the next writes
+    if (j == 0 && sl < nr) acc += (double)lp;
+    // lane i < R takes sample i's value (held by its group's lanes): one 64 B store
+    // from 16 lanes instead of 4 identical copies per sample; lanes >= nr fall
+    // outside the descriptor and are dropped
+    pend_v = __shfl(lp, (lane * G) & 63);
+    pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? (int)nr * 4 : 0);
+  }
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
   if (a.partials) {
     const double sum = block_sum(acc, red);
     if (tid == 0) {

@@ -13,6 +13,16 @@ constexpr bool kFast = NFN_FAST != 0;
 
 template <int G, int DPL, int NV, bool POST>
 void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
+  // contiguous rows, plain chain: the branch-free buffer pipeline (chain_group1_kernel)
+  const bool g1 = !POST && a.t_rowstride == a.P && a.y_bstride * 256 < ((int64_t)1 << 31) &&
+                  (int64_t)(64 / G) * a.P * 4 < ((int64_t)1 << 31) && env_int("NFN_GROUP1", 1) != 0;
+  if (g1) {
+    auto kfn = chain_group1_kernel<G, DPL, kFast, NV>;
+    const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);
+    *grid_out = grid;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+    return;
+  }
   auto kfn = chain_group_kernel<G, DPL, kFast, NV, POST>;
   const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);  // 4 wave teams per WG
   *grid_out = grid;

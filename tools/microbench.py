@@ -97,6 +97,7 @@ def run_grad(cfg, variants, reps=10, rounds=3):
     L = ops.GradLauncher(y, t, ft, d, True, g_out=g)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
+    prewarm(lambda: L.launch(sh))
     times = {v["name"]: [] for v in variants}
     outs = {}
     for r in range(rounds):
@@ -166,6 +167,19 @@ def main():
                         {"name": "tile_v1", "env": {"NFN_GRAD_GROUP": 0}},
                         {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                         {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}])
+        return
+    if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
+        v = [{"name": "group1", "env": {}}, {"name": "group", "env": {"NFN_GROUP1": 0}},
+             {"name": "group1_wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "group1_wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "group1_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "group1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "group1_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "group1_noout", "env": {}, "noout": True},
+             {"name": "group1_b", "env": {}}, {"name": "group_b", "env": {"NFN_GROUP1": 0}}]
+        run("C3", v)
+        run("C2", [{"name": "wave1", "env": {}}, {"name": "generic", "env": {"NFN_WAVE1": 0}},
+                   {"name": "wave1_b", "env": {}}])
         return
     if which[0] == "c3":  # wide-event group kernel
         v = [{"name": "auto_g4x2", "env": {}},
