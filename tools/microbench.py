@@ -153,6 +153,13 @@ def main():
             print(json.dumps({"variant": name, "ms": m, "GBps": nbytes / m / 1e6, "frac8TBs": nbytes / m / 1e6 / 8000}),
                   flush=True)
         return
+    if which[0] == "gradc3":  # C3 backward occupancy: waves per workgroup x register cap
+        run_grad("C3", [{"name": "wpb2", "env": {}},
+                        {"name": "wpb4", "env": {"NFN_GRAD_GROUP_WPB": 4}},
+                        {"name": "wpb2_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+                        {"name": "wpb2_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                        {"name": "wpb2_b", "env": {}}, {"name": "wpb4_b", "env": {"NFN_GRAD_GROUP_WPB": 4}}])
+        return
     if which[0] == "grad":
         v = [{"name": "wave", "env": {}},
              {"name": "wpb4", "env": {"NFN_GRAD_WPB": 4}},

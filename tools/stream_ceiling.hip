@@ -114,6 +114,63 @@ __global__ void __launch_bounds__(256) stream_group_kernel(const float* __restri
   if (acc == 123.456f) sink[threadIdx.x] = acc;
 }
 
+// Backward-shaped stream: read a tile (8 KiB), write a tile (8 KiB) to a second
+// buffer.  ORDER 0: the tile's stores right after its hand-off, BEFORE the next
+// prefetch (the next hand-off waits for them); 1: after the next prefetch (never
+// waited on).  AUX: store cache policy (2 = nt, 0 = default).
+template <int ORDER, int AUX>
+__global__ void __launch_bounds__(256) copy_kernel(const float* __restrict__ t, float* __restrict__ g, int64_t ntiles,
+                                                   float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * 4 + wid, ws = (int64_t)gridDim.x * 4;
+  f32x4 buf[8], cur[8];
+  auto issue = [&](int64_t tile) {
+    const int64_t tc = tile < ntiles ? tile : 0;
+    const auto r = rsrc(t + tc * 2048, tile < ntiles ? 8192 : 0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, k * 1024, 2));
+  };
+  issue(w0);
+  for (int64_t tile = w0; tile < ntiles; tile += ws) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = buf[k] * 1.5f;
+    const auto rg = rsrc(g + tile * 2048, 8192);
+    if (ORDER == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(cur[k], rg, lane * 16, k * 1024, AUX);
+    }
+    issue(tile + ws);
+    if (ORDER == 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(cur[k], rg, lane * 16, k * 1024, AUX);
+    }
+    if (ORDER == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // generic kernel: stores drained per tile
+  }
+  if (cur[0].x == 123.456f) sink[threadIdx.x] = cur[0].y;
+}
+
+template <int ORDER, int AUX>
+float run_copy(const float* t, float* g, int64_t ntiles, float* sink, int grid, int reps) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < reps; ++r) {
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL((copy_kernel<ORDER, AUX>), dim3(grid), dim3(256), 0, 0, t, g, ntiles, sink);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return ts[ts.size() / 2];
+}
+
 template <int G>
 float run_group(const float* t, const float* y, float* out, int64_t ntiles, float* sink, int grid, int reps) {
   hipEvent_t e0, e1;
@@ -173,6 +230,23 @@ int main() {
     hipLaunchKernelGGL(stream_kernel<0>, dim3(cus * 2), dim3(256), 0, 0, t, y, out, ntiles, 0, sink);
   CHECK(hipDeviceSynchronize());
   const double bytes[4] = {(double)tbytes, (double)tbytes + 4.0 * B, (double)tbytes + 8.0 * B, (double)tbytes + 8.0 * B};
+  {
+    float* g2;
+    CHECK(hipMalloc(&g2, tbytes));
+    for (int wpc : {1, 2, 3, 4}) {
+      const int grid = cus * wpc;
+      const double b = 2.0 * (double)tbytes;
+      const float a0 = run_copy<0, 2>(t, g2, ntiles, sink, grid, 10);
+      const float a1 = run_copy<1, 2>(t, g2, ntiles, sink, grid, 10);
+      const float a2 = run_copy<0, 0>(t, g2, ntiles, sink, grid, 10);
+      const float a3 = run_copy<1, 0>(t, g2, ntiles, sink, grid, 10);
+      printf("copy (read 8 KiB + write 8 KiB per tile) wg/CU=%d | drained nt %.4f ms %.0f GB/s | pipelined nt %.4f ms "
+             "%.0f GB/s | drained def %.4f ms %.0f GB/s | pipelined def %.4f ms %.0f GB/s\n",
+             wpc, a0, b / a0 / 1e6, a1, b / a1 / 1e6, a2, b / a2 / 1e6, a3, b / a3 / 1e6);
+      fflush(stdout);
+    }
+    CHECK(hipFree(g2));
+  }
   for (int wpc : {1, 2, 4}) {
     const int grid = cus * wpc;
     const double b = (double)tbytes + 8.0 * B;
