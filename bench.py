@@ -391,7 +391,7 @@ def main():
             kernel_name = "chain_dense_kernel"
             metric = f"Dense(H={args.hidden})->log_prob evals/sec (whole node), {args.config}"
         else:
-            kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group_kernel",
+            kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel",
                            "C5": "chain_persistent_kernel + posterior_merge_kernel"}[args.config]
             metric = ("log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"
                       if args.config == "C2" else f"log_prob evals/sec (whole node), {args.config}")

@@ -78,6 +78,17 @@ for s in $STEPS; do
     c3micro) run c3micro 300 python tools/microbench.py c3 ;;
     dense) run bench_dense 300 python bench.py --mode dense --steps 50 --warmup 10 --cpu-seconds 6 ;;
     densetests) run densetests 300 python -m pytest tests/test_gpu_dense.py -m gpu -q -p no:cacheprovider ;;
+    prof_grad_c3)
+      { cd /tmp; run rocprof_grad_c3 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_grad_c3" -o gradc3 -- \
+        python3 "$ROOT/bench.py" --mode grad --config C3 --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    prof_dense)
+      { cd /tmp; run rocprof_dense 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_dense" -o dense -- \
+        python3 "$ROOT/bench.py" --mode dense --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_c5)
+      { cd /tmp; run pmc_fetch_c5 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_c5" -o f -- \
+        python3 "$ROOT/bench.py" --config C5 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_c5" -o w -- \
+        python3 "$ROOT/bench.py" --config C5 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;

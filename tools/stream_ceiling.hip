@@ -31,7 +31,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes)
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
 }
 
-template <int EXTRA>
+template <int EXTRA, int POL = 2>
 __global__ void __launch_bounds__(256) stream_kernel(const float* __restrict__ t, const float* __restrict__ y,
                                                      float* __restrict__ out, int64_t ntiles, int work,
                                                      float* __restrict__ sink) {
@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(256) stream_kernel(const float* __restrict__ t
 #pragma unroll
     for (int k = 1; k < 8; ++k) s += buf[k];
     float v = s.x + s.y + s.z + s.w + yb;
-    if (EXTRA >= 2) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pv), pr, lane * 4, 0, EXTRA == 2 ? 2 : 0);
+    if (EXTRA >= 2) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pv), pr, lane * 4, 0, EXTRA == 2 ? POL : 0);
     issue(tile + ws);
     for (int i = 0; i < work; ++i) v = fmaf(v, 0.999f, 0.5f);
     acc += v;
@@ -192,6 +192,27 @@ float run_group(const float* t, const float* y, float* out, int64_t ntiles, floa
   return ts[ts.size() / 2];
 }
 
+template <int POL>
+float run_pol(const float* t, const float* y, float* out, int64_t ntiles, float* sink, int grid, int reps) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < reps; ++r) {
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL((stream_kernel<2, POL>), dim3(grid), dim3(256), 0, 0, t, y, out, ntiles, 0, sink);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return ts[ts.size() / 2];
+}
+
 template <int EXTRA>
 float run(const float* t, const float* y, float* out, int64_t ntiles, int work, float* sink, int grid, int reps) {
   hipEvent_t e0, e1;
@@ -230,6 +251,24 @@ int main() {
     hipLaunchKernelGGL(stream_kernel<0>, dim3(cus * 2), dim3(256), 0, 0, t, y, out, ntiles, 0, sink);
   CHECK(hipDeviceSynchronize());
   const double bytes[4] = {(double)tbytes, (double)tbytes + 4.0 * B, (double)tbytes + 8.0 * B, (double)tbytes + 8.0 * B};
+  for (int wpc : {1, 2}) {  // log_prob store cache policy (aux bits: 1 sc0, 2 nt, 16 sc1)
+    const int grid = cus * wpc;
+    const double b = (double)tbytes + 8.0 * B;
+    const int pols[8] = {0, 1, 2, 3, 16, 17, 18, 19};
+    float m[8];
+    m[0] = run_pol<0>(t, y, out, ntiles, sink, grid, 20);
+    m[1] = run_pol<1>(t, y, out, ntiles, sink, grid, 20);
+    m[2] = run_pol<2>(t, y, out, ntiles, sink, grid, 20);
+    m[3] = run_pol<3>(t, y, out, ntiles, sink, grid, 20);
+    m[4] = run_pol<16>(t, y, out, ntiles, sink, grid, 20);
+    m[5] = run_pol<17>(t, y, out, ntiles, sink, grid, 20);
+    m[6] = run_pol<18>(t, y, out, ntiles, sink, grid, 20);
+    m[7] = run_pol<19>(t, y, out, ntiles, sink, grid, 20);
+    printf("t+y+out store policy wg/CU=%d |", wpc);
+    for (int i = 0; i < 8; ++i) printf(" aux%d %.4f ms %.0f GB/s |", pols[i], m[i], b / m[i] / 1e6);
+    printf("\n");
+    fflush(stdout);
+  }
   {
     float* g2;
     CHECK(hipMalloc(&g2, tbytes));
