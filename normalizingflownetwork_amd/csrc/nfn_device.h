@@ -1096,13 +1096,16 @@ __device__ __forceinline__ float gsum(float v) {
 // group touches G consecutive floats).  G trades redundant per-sample scalar
 // work (softplus / tanh / logs are evaluated by every lane of the group) against
 // per-lane vector work (DPL dims each) and tile size.
-template <int G, int DPL, bool FAST>
-__device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int d, int j) {
+// FULL: d == G * DPL (every lane's dimensions exist; config C3), so the per-dimension
+// activity tests and their divergent branches compile away.
+template <int G, int DPL, bool FAST, bool FULL = false>
+__device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int d_, int j) {
+  const int d = FULL ? G * DPL : d_;
   float u[DPL], w[DPL];
   float swu = 0.0f, sww = 0.0f, swz = 0.0f;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    const bool act = j + G * i < d;
+    const bool act = FULL || j + G * i < d;
     u[i] = act ? p[j + G * i] : 0.0f;
     w[i] = act ? p[d + j + G * i] + 1.0f : 0.0f;
     swu += w[i] * u[i];
@@ -1141,15 +1144,16 @@ __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int 
   return f_log<FAST>(fabsf(1.0f + gsum<G>(sd)));
 }
 
-template <int G, int DPL, bool FAST>
-__device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int d, int j) {
+template <int G, int DPL, bool FAST, bool FULL = false>
+__device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int d_, int j) {
+  const int d = FULL ? G * DPL : d_;
   const float alpha = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
   const float beta = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
   float g[DPL];
   float sr = 0.0f;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    const bool act = j + G * i < d;
+    const bool act = FULL || j + G * i < d;
     g[i] = act ? p[2 + j + G * i] : 0.0f;
     sr += act ? fabsf(z[i] - g[i]) : 0.0f;
   }
@@ -1161,7 +1165,7 @@ __device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int 
     const float abh = (alpha * beta) * h;
 #pragma unroll
     for (int i = 0; i < DPL; ++i) {
-      if (j + G * i < d) z[i] = fmaf(abh, z[i] - g[i], z[i]);
+      if (FULL || j + G * i < d) z[i] = fmaf(abh, z[i] - g[i], z[i]);
     }
     const float l2 = fmaf((float)(d - 1), __builtin_amdgcn_logf(1.0f + abh),
                           __builtin_amdgcn_logf(fmaf(abh, alpha * h, 1.0f)));
@@ -1180,7 +1184,7 @@ __device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int 
   const float abh = ab * h;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    if (j + G * i < d) z[i] = z[i] + abh * (z[i] - g[i]);
+    if (FULL || j + G * i < d) z[i] = z[i] + abh * (z[i] - g[i]);
   }
   const float A = 1.0f + abh;
   const float Bv = A + (ab * der_h) * r;
@@ -1195,9 +1199,9 @@ __device__ __forceinline__ int flow_type_at(const uint32_t (&tw)[4], int k) {
   return (int)((w >> (2 * (k & 15))) & 3u);
 }
 
-template <int G, int DPL, bool FAST>
+template <int G, int DPL, bool FAST, bool FULL = false>
 __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row, const ChainArgs& a, int j) {
-  const int d = a.d;
+  const int d = FULL ? G * DPL : a.d;
   const int K = a.prog.K;
   uint32_t tw[4];
 #pragma unroll
@@ -1210,13 +1214,13 @@ __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row
     off -= id == NFN_FLOW_PLANAR ? 2 * d + 1 : (id == NFN_FLOW_RADIAL ? d + 2 : 2 * d);
     const float* p = row + off;
     if (id == NFN_FLOW_PLANAR) {
-      ildj = ildj + planar_gd<G, DPL, FAST>(z, p, d, j);
+      ildj = ildj + planar_gd<G, DPL, FAST, FULL>(z, p, d, j);
     } else if (id == NFN_FLOW_RADIAL) {
-      ildj = ildj + radial_gd<G, DPL, FAST>(z, p, d, j);
+      ildj = ildj + radial_gd<G, DPL, FAST, FULL>(z, p, d, j);
     } else {
 #pragma unroll
       for (int i = 0; i < DPL; ++i) {
-        if (j + G * i < d) {
+        if (FULL || j + G * i < d) {
           const float sc = 1.0f + p[d + j + G * i];
           z[i] = z[i] * sc + p[j + G * i];
           dimterm += f_log<FAST>(fabsf(sc));
@@ -1227,7 +1231,7 @@ __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const int jj = j + G * i;
-    if (jj < d) {
+    if (FULL || jj < d) {
       if (a.trainable) {
         const float sc = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + jj]);
         const float zz = f_div<FAST>(z[i] - row[jj], sc);
@@ -1387,7 +1391,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
 // tile), y and log_prob by buffer instructions too, and no branch between a load
 // and its use: lanes whose slot lies past the tile write their float4 to the pad
 // after the last wave slot.  Plain chain only (the posterior keeps chain_group_kernel).
-template <int G, int DPL, bool FAST, int NV>
+template <int G, int DPL, bool FAST, int NV, bool FULL>
 __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
@@ -1464,7 +1468,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
     issue(tile + ustep);
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
     if (a.prio) __builtin_amdgcn_s_setprio(0);
-    const float lp = eval_chain_gd<G, DPL, FAST>(z, tl + sl * S, a, j) - corr;
+    const float lp = eval_chain_gd<G, DPL, FAST, FULL>(z, tl + sl * S, a, j) - corr;
     wave_lds_sync();  // this tile's LDS reads done before the next writes
     if (j == 0 && sl < nr) acc += (double)lp;
     // lane i < R takes sample i's value (held by its group's lanes): one 64 B store

@@ -17,8 +17,13 @@ void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) 
   const bool g1 = !POST && a.t_rowstride == a.P && a.y_bstride * 256 < ((int64_t)1 << 31) &&
                   (int64_t)(64 / G) * a.P * 4 < ((int64_t)1 << 31) && env_int("NFN_GROUP1", 1) != 0;
   if (g1) {
-    auto kfn = chain_group1_kernel<G, DPL, kFast, NV>;
-    const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);
+    auto kfn = a.d == G * DPL ? chain_group1_kernel<G, DPL, kFast, NV, true>
+                              : chain_group1_kernel<G, DPL, kFast, NV, false>;
+    // 2 resident workgroups per CU (C3: 0.419 vs 0.433 ms at the occupancy limit of
+    // 4, as for the d = 1 kernel: fewer bytes in flight stream faster once the flow
+    // math is short enough to hide); NFN_WG_PER_CU overrides
+    int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);
+    if (env_int("NFN_WG_PER_CU", 0) <= 0) grid = std::min<int64_t>(grid, (int64_t)cu_count() * 2);
     *grid_out = grid;
     hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
     return;

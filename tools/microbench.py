@@ -175,9 +175,21 @@ def main():
                         {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                         {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}])
         return
+    if which[0] == "c5":  # posterior: occupancy x draw split of the generic persistent kernel
+        v = [{"name": "auto", "env": {}},
+             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "split2", "env": {"NFN_POST_SPLIT": 2}}, {"name": "split8", "env": {"NFN_POST_SPLIT": 8}},
+             {"name": "split16", "env": {"NFN_POST_SPLIT": 16}},
+             {"name": "wg2_split8", "env": {"NFN_WG_PER_CU": 2, "NFN_POST_SPLIT": 8}},
+             {"name": "wg3_split8", "env": {"NFN_WG_PER_CU": 3, "NFN_POST_SPLIT": 8}},
+             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "auto_b", "env": {}}]
+        run("C5", v)
+        return
     if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
         v = [{"name": "group1", "env": {}}, {"name": "group", "env": {"NFN_GROUP1": 0}},
-             {"name": "group1_wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "group1_wg4", "env": {"NFN_WG_PER_CU": 4}},
              {"name": "group1_wg3", "env": {"NFN_WG_PER_CU": 3}},
              {"name": "group1_noprio", "env": {"NFN_PRIO": 0}},
              {"name": "group1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
