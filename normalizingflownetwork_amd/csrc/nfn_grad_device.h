@@ -366,14 +366,15 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
 // DPL dimensions j, j + G, ...; inner products are DPP group sums (gsum).
 // ---------------------------------------------------------------------------
 
-template <int G, int DPL, bool FAST>
-__device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d, int j,
+template <int G, int DPL, bool FAST, bool FULL = false>
+__device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d_, int j,
                                               float gl) {
+  const int d = FULL ? G * DPL : d_;
   float u[DPL], w[DPL];
   float swu = 0.0f, sww = 0.0f, swz = 0.0f;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    const bool act = j + G * i < d;
+    const bool act = FULL || j + G * i < d;
     u[i] = act ? p[j + G * i] : 0.0f;
     w[i] = act ? p[d + j + G * i] + 1.0f : 0.0f;
     swu += w[i] * u[i];
@@ -425,7 +426,7 @@ __device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const int jj = j + G * i;
-    if (jj < d) {
+    if (FULL || jj < d) {
       p[jj] = Gv[i] + k1 * w[i];
       p[d + jj] = z[i] * Ss + hpd * uh[i] + cn * Gv[i] - k2 * w[i] + k1 * u[i];
       a[i] = fmaf(w[i], Ss, a[i]);
@@ -434,9 +435,10 @@ __device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[
   if (j == 0) p[2 * d] = Ss;  // the group's lanes read p[2d] above, in lockstep
 }
 
-template <int G, int DPL, bool FAST>
-__device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d, int j,
+template <int G, int DPL, bool FAST, bool FULL = false>
+__device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d_, int j,
                                               float gl) {
+  const int d = FULL ? G * DPL : d_;
   const float xa = 0.3f * p[0] - 2.0f;
   const float xb = 0.1f * p[1] + kLogExpm1One;
   float al, sga, spb, sgb;
@@ -454,7 +456,7 @@ __device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[
   float sr = 0.0f, sda = 0.0f;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
-    dz[i] = j + G * i < d ? z[i] - p[2 + j + G * i] : 0.0f;
+    dz[i] = (FULL || j + G * i < d) ? z[i] - p[2 + j + G * i] : 0.0f;
     sr += fabsf(dz[i]);
     sda += dz[i] * a[i];
   }
@@ -474,7 +476,7 @@ __device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const int jj = j + G * i;
-    if (jj < d) {
+    if (FULL || jj < d) {
       const float sgn = sign0(dz[i]);
       p[2 + jj] = hH * sgn - abh * a[i];
       a[i] = A * a[i] - hH * sgn;
@@ -486,13 +488,14 @@ __device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[
   }
 }
 
-template <int G, int DPL, bool FAST>
-__device__ __forceinline__ void affine_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d, int j,
+template <int G, int DPL, bool FAST, bool FULL = false>
+__device__ __forceinline__ void affine_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* p, int d_, int j,
                                               float gl) {
+  const int d = FULL ? G * DPL : d_;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const int jj = j + G * i;
-    if (jj < d) {
+    if (FULL || jj < d) {
       const float sc = 1.0f + p[d + jj];
       p[jj] = a[i];
       p[d + jj] = z[i] * a[i] + gl * f_div<FAST>(1.0f, sc);
@@ -501,14 +504,15 @@ __device__ __forceinline__ void affine_gd_bwd(const float (&z)[DPL], float (&a)[
   }
 }
 
-template <int G, int DPL, bool FAST>
-__device__ __forceinline__ void base_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* row, int d, int j,
+template <int G, int DPL, bool FAST, bool FULL = false>
+__device__ __forceinline__ void base_gd_bwd(const float (&z)[DPL], float (&a)[DPL], float* row, int d_, int j,
                                             bool trainable, float gl) {
+  const int d = FULL ? G * DPL : d_;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const int jj = j + G * i;
     a[i] = 0.0f;
-    if (jj < d) {
+    if (FULL || jj < d) {
       if (trainable) {
         const float xs = kLogExpm1One + 0.1f * row[d + jj];
         float sps, sgs;

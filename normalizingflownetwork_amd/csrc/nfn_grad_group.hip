@@ -25,7 +25,7 @@ __device__ __forceinline__ int flow_width(int id, int d) {
   return id == NFN_FLOW_PLANAR ? 2 * d + 1 : (id == NFN_FLOW_RADIAL ? d + 2 : 2 * d);
 }
 
-template <int G, int DPL, bool FAST, int NV>
+template <int G, int DPL, bool FAST, int NV, bool FULL>
 __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga) {
   const ChainArgs& a = ga.c;
   extern __shared__ float lds[];
@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
   const int R = 64 / G;
   const int sl = lane / G;
   const int j = lane - sl * G;
-  const int d = a.d;
+  const int d = FULL ? G * DPL : a.d;  // FULL: d == G * DPL (no per-dimension activity tests)
   const int K = a.prog.K;
   const int Q = a.P >> 2;
   const int S = a.lds_stride;
@@ -139,13 +139,13 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
 #pragma unroll
         for (int i = 0; i < DPL; ++i) zh[(k * DPL + i) * 64] = z[i];
         if (id == NFN_FLOW_PLANAR) {
-          ildj = ildj + planar_gd<G, DPL, FAST>(z, p, d, j);
+          ildj = ildj + planar_gd<G, DPL, FAST, FULL>(z, p, d, j);
         } else if (id == NFN_FLOW_RADIAL) {
-          ildj = ildj + radial_gd<G, DPL, FAST>(z, p, d, j);
+          ildj = ildj + radial_gd<G, DPL, FAST, FULL>(z, p, d, j);
         } else {
 #pragma unroll
           for (int i = 0; i < DPL; ++i) {
-            if (j + G * i < d) {
+            if (FULL || j + G * i < d) {
               const float s1 = 1.0f + p[d + j + G * i];
               z[i] = z[i] * s1 + p[j + G * i];
               dimterm += f_log<FAST>(fabsf(s1));
@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
 #pragma unroll
         for (int i = 0; i < DPL; ++i) {
           const int jj = j + G * i;
-          if (jj < d) {
+          if (FULL || jj < d) {
             if (a.trainable) {
               const float s1 = 1e-3f + softplus_tf<FAST>(kLogExpm1One + 0.1f * row[d + jj]);
               const float zz = f_div<FAST>(z[i] - row[jj], s1);
@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
       }
       // reverse pass: flow K-1's block follows the base, flow k-1's follows flow k's
       float adj[DPL];
-      base_gd_bwd<G, DPL, FAST>(z, adj, row, d, j, a.trainable != 0, gl);
+      base_gd_bwd<G, DPL, FAST, FULL>(z, adj, row, d, j, a.trainable != 0, gl);
       off = a.trainable ? 2 * d : 0;
       for (int k = K - 1; k >= 0; --k) {
         const int id = flow_type_at(tw, k);
@@ -182,18 +182,18 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
         for (int i = 0; i < DPL; ++i) zk[i] = zh[(k * DPL + i) * 64];
         float* p = row + off;
         if (id == NFN_FLOW_PLANAR)
-          planar_gd_bwd<G, DPL, FAST>(zk, adj, p, d, j, gl);
+          planar_gd_bwd<G, DPL, FAST, FULL>(zk, adj, p, d, j, gl);
         else if (id == NFN_FLOW_RADIAL)
-          radial_gd_bwd<G, DPL, FAST>(zk, adj, p, d, j, gl);
+          radial_gd_bwd<G, DPL, FAST, FULL>(zk, adj, p, d, j, gl);
         else
-          affine_gd_bwd<G, DPL, FAST>(zk, adj, p, d, j, gl);
+          affine_gd_bwd<G, DPL, FAST, FULL>(zk, adj, p, d, j, gl);
         off += flow_width(id, d);
       }
       if (ga.grad_y) {
 #pragma unroll
         for (int i = 0; i < DPL; ++i) {
           const int jj = j + G * i;
-          if (jj < d) ga.grad_y[(b0 + sl) * d + jj] = a.y_std ? f_div<FAST>(adj[i], a.y_std[jj]) : adj[i];
+          if (FULL || jj < d) ga.grad_y[(b0 + sl) * d + jj] = a.y_std ? f_div<FAST>(adj[i], a.y_std[jj]) : adj[i];
         }
       }
     }
@@ -227,11 +227,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
 
 template <int G, int DPL, int NV>
 void launch_gg(const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid_out) {
-  // Two-wave workgroups: finer LDS allocation granules (C3: 1.226 vs 1.250 ms with
-  // four); a register cap at 3 waves per SIMD spills (2.07 ms).  NFN_GRAD_GROUP_WPB=4
-  // restores four-wave groups.
-  auto kfn = chain_grad_group_kernel<G, DPL, kFast, NV>;
-  const int wpb = env_int("NFN_GRAD_GROUP_WPB", 2) == 4 ? 4 : 2;
+  // Four-wave workgroups (C3 with the FULL specialisation: 1.004-1.018 ms vs
+  // 1.007-1.068 with two; two-wave groups had won by 2.5 % before it); a register
+  // cap at 3 waves per SIMD spills (2.07 ms).  NFN_GRAD_GROUP_WPB=2 for two.
+  auto kfn = ga.c.d == G * DPL ? chain_grad_group_kernel<G, DPL, kFast, NV, true>
+                                : chain_grad_group_kernel<G, DPL, kFast, NV, false>;
+  const int wpb = env_int("NFN_GRAD_GROUP_WPB", 4) == 2 ? 2 : 4;
   const size_t lds_b = lds / 4 * wpb;  // `lds` holds four wave slots
   const int T = 64 * wpb;
   const int64_t grid = persistent_grid(kfn, T, lds_b, (ga.c.ntiles + wpb - 1) / wpb);
