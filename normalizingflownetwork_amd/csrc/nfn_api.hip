@@ -221,8 +221,10 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     const int R = 64 / G;  // samples per wave tile
     a.lds_stride = group_lds_stride(P, G);
     a.ntiles = (B + R - 1) / R;
-    // four wave slots; + pad: inactive lanes may read G * DPL floats past a row's block
-    const size_t lds = (size_t)(kMaxBlock / 64) * R * a.lds_stride * sizeof(float) + (G * DPL + 4) * sizeof(float);
+    // four wave slots + pad: inactive lanes may read G * DPL floats past a row's block,
+    // and the contiguous-row kernel parks out-of-tile float4 slots there (one per lane)
+    const size_t lds = (size_t)(kMaxBlock / 64) * R * a.lds_stride * sizeof(float) +
+                       std::max<size_t>((G * DPL + 4) * sizeof(float), 64 * 16);
     launched_group = use_fast_math() ? launch_group_fast(posterior, G, DPL, nv_group, a, lds, s, &nblk)
                                      : launch_group_precise(posterior, G, DPL, nv_group, a, lds, s, &nblk);
     if (!launched_group) a.lds_stride = g.lds_stride;

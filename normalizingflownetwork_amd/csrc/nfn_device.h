@@ -1389,8 +1389,8 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
 // contiguous block streamed by buffer loads at lane-linear offsets through a
 // descriptor bounded at B (zeros past the end, empty descriptors past the last
 // tile), y and log_prob by buffer instructions too, and no branch between a load
-// and its use: lanes whose slot lies past the tile write their float4 to the pad
-// after the last wave slot.  Plain chain only (the posterior keeps chain_group_kernel).
+// and its use: lanes whose slot lies past the tile write their float4 to a per-lane
+// pad after the last wave slot (distinct addresses: no same-address write conflicts).  Plain chain only (the posterior keeps chain_group_kernel).
 template <int G, int DPL, bool FAST, int NV, bool FULL>
 __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
@@ -1406,7 +1406,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   const int S = a.lds_stride;
   const int nslots = R * Q;  // float4 pieces per tile
   float* tl = lds + wid * R * S;
-  float* pad = lds + (kMaxBlock / 64) * R * S;  // scratch for out-of-tile slots
+  float* pad = lds + (kMaxBlock / 64) * R * S + 4 * lane;  // per-lane scratch for out-of-tile slots
   int loff[NV];  // LDS float offset of this lane's slot k (tile-invariant)
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
