@@ -899,12 +899,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <bool FAST, int Q, int G, bool PACKED>
+template <bool FAST, int Q, bool PACKED>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
-  static_assert(G == 1 || G == 4, "tiles per unit: 1 or 4");
   extern __shared__ float lds[];
   __shared__ double red[kMaxBlock / 64];
-  __shared__ float obuf[G == 4 ? (kMaxBlock / 64) * 256 : 1];  // per wave: a unit's log_prob
   constexpr int RSTEP = 64 / Q;  // rows per wave-instruction
   constexpr int kNT = 2;         // buffer cache policy: non-temporal (streamed once)
   const int tid = threadIdx.x;
@@ -913,10 +911,8 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   const int64_t rs = a.t_rowstride;
   const int r0 = lane / Q, c4 = lane % Q;
   float* tl = lds + wid * 64 * S;
-  float* ob = obuf + (G == 4 ? wid * 256 : 0);
   const int l0 = r0 * S + 4 * c4;
   const int64_t ntiles = a.ntiles;
-  const int64_t nunits = (ntiles + G - 1) / G;  // a unit = G consecutive 64-row tiles
   const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
   const bool norm = a.y_mean != nullptr;
@@ -927,7 +923,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     corr = f_log<FAST>(ystd);
   }
   // diagnostic (NFN_ABLATE_LOADS): every tile re-reads the wave's first tile
-  const int64_t abl_tile = a.ablate_loads ? u0 * G : -1;
+  const int64_t abl_tile = a.ablate_loads ? u0 : -1;
   // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
   const int yoff = lane * (int)a.y_bstride * 4;
   const int toff = (r0 * (int)rs + 4 * c4) * 4;
@@ -952,63 +948,44 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   };
 
   double acc = 0.0;
-  // The previous unit's log_prob, stored through a descriptor bounded at B (empty
-  // before the first unit: the store is always issued).  It is issued right AFTER
-  // the next prefetch, so the next hand-off's wait does not cover it; with G = 4 a
-  // unit's 256 values leave as one contiguous 1 KiB store (float4 per lane) per 4
-  // tiles instead of four 256-byte stores.
+  // The previous tile's log_prob, stored through a descriptor bounded at B (empty
+  // before the first tile: the store is always issued).  It is issued right AFTER
+  // the next prefetch, so the next hand-off's wait (vmcnt(1)) does not cover it.
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
-  float4 pend_v = make_float4(0.f, 0.f, 0.f, 0.f);
+  float pend_v = 0.0f;
   auto flush = [&]() {
-    if constexpr (G == 4)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, pend_v), pend_r, lane * 16, 0, kNT);
-    else
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v.x), pend_r, lane * 4, 0, kNT);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
   };
-  issue(u0 * G);
+  issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
-  for (int64_t unit = u0; unit < nunits; unit += ustep) {
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int64_t tile = unit * G + g;  // may be past the end in the last unit (empty)
-      const int64_t b0 = tile * 64;
-      const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
-      if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
-#pragma unroll
-      for (int k = 0; k < Q; ++k) {
-        float* dst = tl + l0 + k * RSTEP * S;
-        dst[0] = buf[k].x;
-        dst[1] = buf[k].y;
-        dst[2] = buf[k].z;
-        dst[3] = buf[k].w;
-      }
-      const float z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
-      wave_lds_sync();
-      issue(g + 1 < G ? tile + 1 : (unit + ustep) * G);
-      if (g == 0) flush();
-      if (a.prio) __builtin_amdgcn_s_setprio(0);
-      float lp;
-      if constexpr (FAST) {
-        lp = eval_chain1_fast<PACKED>(z0, tl + lane * S, a) - corr;
-      } else {
-        float z[1] = {z0};
-        lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
-      }
-      if (lane < nr) acc += (double)lp;
-      if constexpr (G == 4) {
-        ob[g * 64 + lane] = lp;
-      } else {
-        pend_v.x = lp;
-        pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
-      }
-      wave_lds_sync();  // this tile's LDS reads done before the next writes
+    for (int k = 0; k < Q; ++k) {
+      float* dst = tl + l0 + k * RSTEP * S;
+      dst[0] = buf[k].x;
+      dst[1] = buf[k].y;
+      dst[2] = buf[k].z;
+      dst[3] = buf[k].w;
     }
-    if constexpr (G == 4) {
-      pend_v = *reinterpret_cast<const float4*>(ob + 4 * lane);
-      const int64_t ub = unit * 256;
-      const int64_t nu = max((int64_t)0, min((int64_t)256, a.B - ub));
-      pend_r = tile_rsrc(a.out && nu > 0 ? a.out + ub : a.out, a.out ? nu * 4 : 0);
+    const float z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
+    wave_lds_sync();
+    issue(tile + ustep);
+    flush();
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
+    float lp;
+    if constexpr (FAST) {
+      lp = eval_chain1_fast<PACKED>(z0, tl + lane * S, a) - corr;
+    } else {
+      float z[1] = {z0};
+      lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
     }
+    if (lane < nr) acc += (double)lp;
+    pend_v = lp;
+    pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+    wave_lds_sync();  // this tile's LDS reads done before the next writes
   }
   flush();
   if (a.partials) {

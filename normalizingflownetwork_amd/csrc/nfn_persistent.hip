@@ -11,14 +11,12 @@ namespace {
 
 constexpr bool kFast = NFN_FAST != 0;
 
-// d = 1 wave-tile kernel (chain_wave1_kernel) for rows of exactly Q float4, units of
-// G tiles per wave step.
-template <int Q, int G>
+// d = 1 wave-tile kernel (chain_wave1_kernel) for rows of exactly Q float4.
+template <int Q>
 void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
-  auto kfn = (kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1)
-                 ? chain_wave1_kernel<kFast, Q, G, kFast>
-                 : chain_wave1_kernel<kFast, Q, G, false>;
-  const int64_t units = (a.ntiles + G - 1) / G;
+  auto kfn = (kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? chain_wave1_kernel<kFast, Q, kFast>
+                                                                        : chain_wave1_kernel<kFast, Q, false>;
+  const int64_t units = a.ntiles;
   const int teams = T / 64;
   // Resident workgroups per CU: a long chain (C2: 10 flows) keeps each wave busy
   // long enough that 2 waves per SIMD hide the streamed rows and fewer bytes in
@@ -33,14 +31,6 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }
 
-template <int Q>
-void launch_w1_d(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
-  if (env_int("NFN_UNIT_TILES", 1) == 1)
-    launch_w1<Q, 1>(a, T, lds, s, g);
-  else
-    launch_w1<Q, 4>(a, T, lds, s, g);
-}
-
 template <bool POST>
 bool try_wave1(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
   // the posterior (C5) stays on the generic kernel: measured 0.177 vs 0.181 ms there
@@ -48,10 +38,10 @@ bool try_wave1(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int6
   // 32-bit lane byte offsets: a tile's 64 rows (and y entries) must span < 2 GiB
   if (a.t_rowstride * 256 >= (int64_t)1 << 31 || a.y_bstride * 256 >= (int64_t)1 << 31) return false;
   switch (Q) {
-    case 2: launch_w1_d<2>(a, T, lds, s, g); return true;
-    case 4: launch_w1_d<4>(a, T, lds, s, g); return true;
-    case 8: launch_w1_d<8>(a, T, lds, s, g); return true;
-    case 16: launch_w1_d<16>(a, T, lds, s, g); return true;
+    case 2: launch_w1<2>(a, T, lds, s, g); return true;
+    case 4: launch_w1<4>(a, T, lds, s, g); return true;
+    case 8: launch_w1<8>(a, T, lds, s, g); return true;
+    case 16: launch_w1<16>(a, T, lds, s, g); return true;
     default: return false;
   }
 }

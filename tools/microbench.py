@@ -153,6 +153,14 @@ def main():
             print(json.dumps({"variant": name, "ms": m, "GBps": nbytes / m / 1e6, "frac8TBs": nbytes / m / 1e6 / 8000}),
                   flush=True)
         return
+    if which[0] == "gradc2":  # C2 backward occupancy: waves per workgroup x resident workgroups
+        v = [{"name": "auto", "env": {}}]
+        for wpb in (2, 4):
+            for wg in (1, 2, 3, 4, 6):
+                v.append({"name": f"wpb{wpb}_wg{wg}", "env": {"NFN_GRAD_WPB": wpb, "NFN_WG_PER_CU": wg}})
+        v.append({"name": "auto_b", "env": {}})
+        run_grad("C2", v, reps=8, rounds=2)
+        return
     if which[0] == "gradc3":  # C3 backward occupancy: waves per workgroup x register cap
         run_grad("C3", [{"name": "wpb4", "env": {}},
                         {"name": "wpb2", "env": {"NFN_GRAD_GROUP_WPB": 2}},
@@ -174,6 +182,90 @@ def main():
                         {"name": "tile_v1", "env": {"NFN_GRAD_GROUP": 0}},
                         {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                         {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}])
+        return
+    if which[0] == "c5":  # posterior: occupancy x draw split of the generic persistent kernel
+        v = [{"name": "auto", "env": {}},
+             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "split2", "env": {"NFN_POST_SPLIT": 2}}, {"name": "split8", "env": {"NFN_POST_SPLIT": 8}},
+             {"name": "split16", "env": {"NFN_POST_SPLIT": 16}},
+             {"name": "wg2_split8", "env": {"NFN_WG_PER_CU": 2, "NFN_POST_SPLIT": 8}},
+             {"name": "wg3_split8", "env": {"NFN_WG_PER_CU": 3, "NFN_POST_SPLIT": 8}},
+             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "auto_b", "env": {}}]
+        run("C5", v)
+        return
+    if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
+        v = [{"name": "group1", "env": {}}, {"name": "group", "env": {"NFN_GROUP1": 0}},
+             {"name": "group1_wg4", "env": {"NFN_WG_PER_CU": 4}},
+             {"name": "group1_wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "group1_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "group1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "group1_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "group1_noout", "env": {}, "noout": True},
+             {"name": "group1_b", "env": {}}, {"name": "group_b", "env": {"NFN_GROUP1": 0}}]
+        run("C3", v)
+        run("C2", [{"name": "wave1", "env": {}}, {"name": "generic", "env": {"NFN_WAVE1": 0}},
+                   {"name": "wave1_b", "env": {}}])
+        return
+    if which[0] == "c3":  # wide-event group kernel
+        v = [{"name": "auto_g4x2", "env": {}},
+             {"name": "g8x1", "env": {"NFN_GROUP_LANES": 8}},
+             {"name": "g2x4", "env": {"NFN_GROUP_LANES": 2}},
+             {"name": "tile", "env": {"NFN_LOAD_MODE": "tile"}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "g8_compute_only", "env": {"NFN_GROUP_LANES": 8, "NFN_ABLATE_LOADS": 1}},
+             {"name": "g2_compute_only", "env": {"NFN_GROUP_LANES": 2, "NFN_ABLATE_LOADS": 1}},
+             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}},
+             {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "precise", "env": {}, "math": "precise"}]
+        run("C3", v)
+        return
+    if which[0] == "prio":  # wave priority around the tile hand-off
+        v = [{"name": "prio", "env": {"NFN_PRIO": 1}}, {"name": "noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "prio_b", "env": {"NFN_PRIO": 1}}, {"name": "noprio_b", "env": {"NFN_PRIO": 0}}]
+        for cfg in ("C2", "C5"):
+            run(cfg, v, reps=30, rounds=4)
+        return
+    if which[0] == "valu":  # compute vs memory floors
+        for cfg in ("C2", "C5"):
+            W = {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}
+            v = [{"name": "wave", "env": dict(W)},
+                 {"name": "compute_only", "env": dict(W, NFN_ABLATE_LOADS=1)},
+                 {"name": "memory_only", "env": dict(W, NFN_ABLATE_FLOWS=1)},
+                 {"name": "precise", "env": dict(W), "math": "precise"},
+                 {"name": "precise_compute_only", "env": dict(W, NFN_ABLATE_LOADS=1), "math": "precise"}]
+            run(cfg, v)
+        return
+    if which[0] == "mode":  # load-mode study, C2 and C5
+        for cfg in ("C2", "C5"):
+            v = [{"name": "coop", "env": {"NFN_LOAD_MODE": "coop"}},
+                 {"name": "wave", "env": {"NFN_LOAD_MODE": "wave"}},
+                 {"name": "coop_ntst", "env": {"NFN_LOAD_MODE": "coop", "NFN_NT_STORES": 1}},
+                 {"name": "wave_ntst", "env": {"NFN_LOAD_MODE": "wave", "NFN_NT_STORES": 1}},
+                 {"name": "coop_wg3", "env": {"NFN_LOAD_MODE": "coop", "NFN_WG_PER_CU": 3}},
+                 {"name": "wave_wg3", "env": {"NFN_LOAD_MODE": "wave", "NFN_WG_PER_CU": 3}},
+                 {"name": "wave_wg2", "env": {"NFN_LOAD_MODE": "wave", "NFN_WG_PER_CU": 2}},
+                 {"name": "coop_nont", "env": {"NFN_LOAD_MODE": "coop", "NFN_NT_LOADS": 0}},
+                 {"name": "wave_ablate", "env": {"NFN_LOAD_MODE": "wave", "NFN_ABLATE_FLOWS": 1}},
+                 {"name": "coop_ablate", "env": {"NFN_LOAD_MODE": "coop", "NFN_ABLATE_FLOWS": 1}}]
+            if cfg == "C5":
+                v += [{"name": "coop_nosplit", "env": {"NFN_LOAD_MODE": "coop", "NFN_POST_SPLIT": 1}},
+                      {"name": "wave_nosplit", "env": {"NFN_LOAD_MODE": "wave", "NFN_POST_SPLIT": 1}}]
+            run(cfg, v)
+        return
+    if which[0] == "wave1":  # straight-line d = 1 wave kernel: occupancy, output, ablations
+        v = [{"name": "wave1", "env": {}}, {"name": "generic", "env": {"NFN_WAVE1": 0}},
+             {"name": "wave1_wg3", "env": {"NFN_WG_PER_CU": 3}},
+             {"name": "wave1_wg4", "env": {"NFN_WG_PER_CU": 4}},
+             {"name": "wave1_noout", "env": {}, "noout": True},
+             {"name": "wave1_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "wave1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": 2}},
+             {"name": "wave1_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "wave1_b", "env": {}}]
+        for cfg in which[1:] or ["C2", "C1"]:
+            run(cfg, v)
         return
     if which[0] == "c5":  # posterior: occupancy x draw split of the generic persistent kernel
         v = [{"name": "auto", "env": {}},
