@@ -142,6 +142,138 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
   }
 }
 
+// d = 1, fast math: chain_dense_kernel with chain_wave1_kernel's memory pipeline —
+// the tile's h rows and y through buffer descriptors bounded at B (tiles past the
+// end empty), one counted wait per hand-off, the previous tile's log_prob stored
+// after the next prefetch, no branch between a load and its use.  QH = H / 4.
+template <int QH>
+__global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  constexpr int H = 4 * QH;
+  constexpr int RSTEP = 64 / QH;  // h rows per wave-instruction
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int SH = da.h_lds_stride;  // odd
+  const int S = a.lds_stride;      // odd, >= P
+  const int P = a.P;
+  const int NN = (P + 15) >> 4;    // 16-column N tiles
+  const int NP = NN * 16;
+  float* wl = lds;
+  float* hl = lds + H * NP + wid * (64 * SH + 64 * S);
+  float* tl = hl + 64 * SH;
+  for (int i = tid; i < H * NP; i += blockDim.x) {
+    const int k = i / NP, n = i - (i / NP) * NP;
+    wl[i] = n < P ? da.W[(int64_t)k * P + n] : 0.0f;
+  }
+  __syncthreads();
+  const int r0 = lane / QH, c4 = lane % QH;
+  const int l0 = r0 * SH + 4 * c4;
+  const int64_t hs = da.h_rowstride;
+  const int64_t ntiles = a.ntiles;
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int hoff = (r0 * (int)hs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)hs * 4;
+  float4 buf[QH];
+  float ybuf;
+  auto issue = [&](int64_t tile) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const auto rh = tile_rsrc(da.h + b0c * hs, nr > 0 ? ((nr - 1) * hs + H) * 4 : 0);
+#pragma unroll
+    for (int k = 0; k < QH; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, k * kstep, kNT));
+  };
+  double acc_sum = 0.0;
+  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
+  float pend_v = 0.0f;
+  auto flush = [&]() {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  };
+  issue(u0);
+  flush();  // empty: every path into the loop ends [loads][store] (counted waits)
+  const int am = lane & 15;  // A row within an M tile / B and C column
+  const int ak = lane >> 4;  // A column (k) within a k-step / B row / C row quad
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+#pragma unroll
+    for (int k = 0; k < QH; ++k) {
+      float* dst = hl + l0 + k * RSTEP * SH;
+      dst[0] = buf[k].x;
+      dst[1] = buf[k].y;
+      dst[2] = buf[k].z;
+      dst[3] = buf[k].w;
+    }
+    const float z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+    wave_lds_sync();
+    issue(tile + ustep);
+    flush();
+    // t = h W + b on the matrix cores, 16 columns at a time (exact fp32)
+    for (int nt = 0; nt < NN; ++nt) {
+      f32x4v acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < QH; ++ks) {
+        const float bv = wl[(4 * ks + ak) * NP + 16 * nt + am];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const float av = hl[(16 * mt + am) * SH + 4 * ks + ak];
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mt], 0, 0, 0);
+        }
+      }
+      const int n = 16 * nt + am;
+      if (n < P) {
+        const float bn = da.bias ? da.bias[n] : 0.0f;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tl[(16 * mt + 4 * ak + i) * S + n] = acc[mt][i] + bn;
+        }
+      }
+    }
+    wave_lds_sync();
+    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true>(z0, tl + lane * S, a)
+                                     : eval_chain1_fast<false>(z0, tl + lane * S, a)) - corr;
+    if (lane < nr) acc_sum += (double)lp;
+    pend_v = lp;
+    pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+    wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
+  }
+  flush();
+  if (a.partials) {
+    const double sum = block_sum(acc_sum, red);
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
+
+template <int QH>
+void launch_d1(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = chain_dense1_kernel<QH>;
+  int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+}
+
 template <int DM, bool FAST, int NVH>
 void launch_d(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out) {
   auto kfn = chain_dense_kernel<DM, FAST, NVH>;
@@ -164,6 +296,19 @@ bool launch_d_h(int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t
 
 template <bool FAST>
 bool launch_d_dm(int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* g) {
+  const ChainArgs& a = da.c;
+  if constexpr (FAST) {
+    if (dm == 1 && a.d == 1 && env_int("NFN_DENSE1", 1) != 0 && da.h_rowstride * 256 < ((int64_t)1 << 31) &&
+        a.y_bstride * 256 < ((int64_t)1 << 31)) {
+      switch (nvh) {
+        case 1: launch_d1<1>(da, lds, s, g); return true;
+        case 2: launch_d1<2>(da, lds, s, g); return true;
+        case 4: launch_d1<4>(da, lds, s, g); return true;
+        case 8: launch_d1<8>(da, lds, s, g); return true;
+        case 16: launch_d1<16>(da, lds, s, g); return true;
+      }
+    }
+  }
   switch (dm) {
     case 1: return launch_d_h<1, FAST>(nvh, da, lds, s, g);
     case 2: return launch_d_h<2, FAST>(nvh, da, lds, s, g);

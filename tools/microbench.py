@@ -128,6 +128,47 @@ def run_grad(cfg, variants, reps=10, rounds=3):
                           "rounds_ms": times[v["name"]]}), flush=True)
 
 
+def run_dense(variants, H=16, reps=20, rounds=3):
+    """Fused Dense -> chain (C2 flows, d = 1) variants, same interleaving."""
+    ft, d, B, _ = CFG["C2"]
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    h = torch.randn((B, H), generator=gen, device="cuda")
+    W = torch.randn((H, P), generator=gen, device="cuda") / float(np.sqrt(H))
+    b = 0.1 * torch.randn((P,), generator=gen, device="cuda")
+    L = ops.DenseLauncher(y, h, W, b, ft, d, True)
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    prewarm(lambda: L.launch(sh))
+    times = {v["name"]: [] for v in variants}
+    outs = {}
+    for r in range(rounds):
+        for v in variants:
+            for k, val in v.get("env", {}).items():
+                os.environ[k] = str(val)
+            for _ in range(3):
+                L.launch(sh)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in evs:
+                e0.record(stream)
+                L.launch(sh)
+                e1.record(stream)
+            torch.cuda.synchronize()
+            times[v["name"]].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+            if r == 0:
+                outs[v["name"]] = L.out.clone()
+            for k in v.get("env", {}):
+                os.environ.pop(k, None)
+    ref = outs[variants[0]["name"]]
+    for v in variants:
+        ms = float(np.median(times[v["name"]]))
+        print(json.dumps({"cfg": "C2", "mode": "dense", "H": H, "variant": v["name"], "ms": ms,
+                          "evals_per_s": B / ms * 1e3,
+                          "maxdiff_vs_first": float((outs[v["name"]] - ref).abs().max().item()),
+                          "rounds_ms": times[v["name"]]}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
     if which[0] == "ceiling":  # HBM ceilings of plain torch streams over the C2 parameter buffer
@@ -152,6 +193,13 @@ def main():
             m = float(np.median(ms))
             print(json.dumps({"variant": name, "ms": m, "GBps": nbytes / m / 1e6, "frac8TBs": nbytes / m / 1e6 / 8000}),
                   flush=True)
+        return
+    if which[0] == "dense":  # fused Dense -> chain: wave1-style pipeline vs generic, occupancy
+        run_dense([{"name": "dense1", "env": {}}, {"name": "generic", "env": {"NFN_DENSE1": 0}},
+                   {"name": "dense1_wg2", "env": {"NFN_WG_PER_CU": 2}},
+                   {"name": "dense1_wg3", "env": {"NFN_WG_PER_CU": 3}},
+                   {"name": "dense1_nochain", "env": {"NFN_ABLATE_FLOWS": 1}},
+                   {"name": "dense1_b", "env": {}}, {"name": "generic_b", "env": {"NFN_DENSE1": 0}}])
         return
     if which[0] == "gradc2":  # C2 backward occupancy: waves per workgroup x resident workgroups
         v = [{"name": "auto", "env": {}}]
