@@ -146,7 +146,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
 // the tile's h rows and y through buffer descriptors bounded at B (tiles past the
 // end empty), one counted wait per hand-off, the previous tile's log_prob stored
 // after the next prefetch, no branch between a load and its use.  QH = H / 4.
-template <int QH>
+// NN = 16-column N tiles of t (P <= 16 NN), a compile-time count so the GEMM unrolls
+// and the tile's A fragments are read from LDS once for all N tiles.
+template <int QH, int NN>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
@@ -160,8 +162,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   const int SH = da.h_lds_stride;  // odd
   const int S = a.lds_stride;      // odd, >= P
   const int P = a.P;
-  const int NN = (P + 15) >> 4;    // 16-column N tiles
-  const int NP = NN * 16;
+  constexpr int NP = NN * 16;
   float* wl = lds;
   float* hl = lds + H * NP + wid * (64 * SH + 64 * S);
   float* tl = hl + 64 * SH;
@@ -224,7 +225,14 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
     wave_lds_sync();
     issue(tile + ustep);
     flush();
-    // t = h W + b on the matrix cores, 16 columns at a time (exact fp32)
+    // t = h W + b on the matrix cores, 16 columns at a time (exact fp32); the A
+    // fragments (4 M tiles x QH k-steps) are shared by every N tile
+    float av[4][QH];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < QH; ++ks) av[mt][ks] = hl[(16 * mt + am) * SH + 4 * ks + ak];
+#pragma unroll
     for (int nt = 0; nt < NN; ++nt) {
       f32x4v acc[4];
 #pragma unroll
@@ -233,10 +241,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
       for (int ks = 0; ks < QH; ++ks) {
         const float bv = wl[(4 * ks + ak) * NP + 16 * nt + am];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const float av = hl[(16 * mt + am) * SH + 4 * ks + ak];
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mt], 0, 0, 0);
-        }
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][ks], bv, acc[mt], 0, 0, 0);
       }
       const int n = 16 * nt + am;
       if (n < P) {
@@ -268,7 +273,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
 
 template <int QH>
 void launch_d1(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out) {
-  auto kfn = chain_dense1_kernel<QH>;
+  const int nn = (da.c.P + 15) >> 4;
+  auto kfn = nn <= 1 ? chain_dense1_kernel<QH, 1>
+                     : (nn == 2 ? chain_dense1_kernel<QH, 2> : (nn == 3 ? chain_dense1_kernel<QH, 3>
+                                                                       : chain_dense1_kernel<QH, 4>));
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
@@ -305,7 +313,6 @@ bool launch_d_dm(int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s
         case 2: launch_d1<2>(da, lds, s, g); return true;
         case 4: launch_d1<4>(da, lds, s, g); return true;
         case 8: launch_d1<8>(da, lds, s, g); return true;
-        case 16: launch_d1<16>(da, lds, s, g); return true;
       }
     }
   }
