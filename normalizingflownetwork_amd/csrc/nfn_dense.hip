@@ -173,6 +173,17 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   __syncthreads();
   const int r0 = lane / QH, c4 = lane % QH;
   const int l0 = r0 * SH + 4 * c4;
+  const int am = lane & 15;  // A row within an M tile / B and C column
+  const int ak = lane >> 4;  // A column (k) within a k-step / B row / C row quad
+  // B fragments (W) stay in registers for the whole launch when they are few
+  constexpr bool kBReg = QH * NN <= 16;
+  float bvr[kBReg ? QH : 1][kBReg ? NN : 1];
+  if constexpr (kBReg) {
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt) bvr[ks][nt] = wl[(4 * ks + ak) * NP + 16 * nt + am];
+  }
   const int64_t hs = da.h_rowstride;
   const int64_t ntiles = a.ntiles;
   const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
@@ -208,8 +219,6 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   };
   issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
-  const int am = lane & 15;  // A row within an M tile / B and C column
-  const int ak = lane >> 4;  // A column (k) within a k-step / B row / C row quad
   for (int64_t tile = u0; tile < ntiles; tile += ustep) {
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
@@ -239,7 +248,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
       for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int ks = 0; ks < QH; ++ks) {
-        const float bv = wl[(4 * ks + ak) * NP + 16 * nt + am];
+        const float bv = kBReg ? bvr[kBReg ? ks : 0][kBReg ? nt : 0] : wl[(4 * ks + ak) * NP + 16 * nt + am];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][ks], bv, acc[mt], 0, 0, 0);
       }
