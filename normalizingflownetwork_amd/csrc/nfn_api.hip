@@ -420,6 +420,8 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   da.H = H;
   da.h_lds_stride = H | 1;
   const int NP = ((P + 15) / 16) * 16;
+  // generic kernel: per wave the h tile + a row-major 64 x S t tile (chain_dense1_kernel
+  // sizes its own, smaller, overlaid region)
   const size_t lds = (size_t)(H * NP + 4 * (64 * da.h_lds_stride + 64 * a.lds_stride) + 16) * sizeof(float);
   int64_t grid = 0;
   if (!launch_dense(use_fast_math(), dm_for(d), H / 4, da, lds, s, &grid))

@@ -160,12 +160,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int SH = da.h_lds_stride;  // odd
-  const int S = a.lds_stride;      // odd, >= P
   const int P = a.P;
   constexpr int NP = NN * 16;
+  // t tile column-major at the padded column stride kCS (== 4 mod 32 dwords: the
+  // MFMA results leave as conflict-free ds_write_b128 of 4 rows, and the chain's
+  // per-lane reads of one column are consecutive), one spare column for the packed
+  // chain's read-ahead, overlaying the h tile: a wave's t writes follow its own A
+  // fragment reads of h in LDS program order
   float* wl = lds;
-  float* hl = lds + H * NP + wid * (64 * SH + 64 * S);
-  float* tl = hl + 64 * SH;
+  float* hl = lds + H * NP + wid * dense1_wave_floats(P, SH);
+  float* tl = hl;
   for (int i = tid; i < H * NP; i += blockDim.x) {
     const int k = i / NP, n = i - (i / NP) * NP;
     wl[i] = n < P ? da.W[(int64_t)k * P + n] : 0.0f;
@@ -256,15 +260,13 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
       if (n < P) {
         const float bn = da.bias ? da.bias[n] : 0.0f;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) tl[(16 * mt + 4 * ak + i) * S + n] = acc[mt][i] + bn;
-        }
+        for (int mt = 0; mt < 4; ++mt)
+          *reinterpret_cast<f32x4v*>(tl + n * kCS + 16 * mt + 4 * ak) = acc[mt] + bn;
       }
     }
     wave_lds_sync();
-    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true>(z0, tl + lane * S, a)
-                                     : eval_chain1_fast<false>(z0, tl + lane * S, a)) - corr;
+    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS>(z0, tl + lane, a)
+                                     : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
     if (lane < nr) acc_sum += (double)lp;
     pend_v = lp;
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
@@ -281,8 +283,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
 }
 
 template <int QH>
-void launch_d1(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out) {
+void launch_d1(const DenseArgs& da, size_t /*generic kernel's LDS*/, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
+  const size_t lds = (size_t)(4 * QH * nn * 16 + 4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
   auto kfn = nn <= 1 ? chain_dense1_kernel<QH, 1>
                      : (nn == 2 ? chain_dense1_kernel<QH, 2> : (nn == 3 ? chain_dense1_kernel<QH, 3>
                                                                        : chain_dense1_kernel<QH, 4>));

@@ -430,11 +430,14 @@ __device__ __forceinline__ float affine1_fast(float& z, float sh, float scraw) {
   return sc;
 }
 
+// ST: floats between consecutive parameters of one sample (1 = row-major tile; the
+// fused Dense kernel's column-major t tile uses its padded column stride).
+template <int ST = 1>
 __device__ __forceinline__ void read3(float (&v)[3], const float* row, int st) {
-  const float* p = row + (st >> 2);
+  const float* p = row + (st >> 2) * ST;
   v[0] = p[0];
-  v[1] = p[1];
-  v[2] = (st & 3) == NFN_FLOW_AFFINE ? 0.0f : p[2];
+  v[1] = p[ST];
+  v[2] = (st & 3) == NFN_FLOW_AFFINE ? 0.0f : p[2 * ST];
 }
 
 // Chains of up to 16 flows: the flow types are packed 2 bits per flow in one
@@ -451,12 +454,14 @@ __device__ __forceinline__ float flow1_fast(int id, float& z, const float (&p)[3
   return affine1_fast(z, p[0], p[1]);
 }
 
+template <int ST = 1>
 __device__ __forceinline__ void read3c(float (&v)[3], const float* row, int off) {
-  v[0] = row[off];
-  v[1] = row[off + 1];
-  v[2] = row[off + 2];
+  v[0] = row[off * ST];
+  v[1] = row[(off + 1) * ST];
+  v[2] = row[(off + 2) * ST];
 }
 
+template <int ST = 1>
 __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, uint32_t types, int K, int P) {
   float l2 = 0.0f;
   int id = (int)(types & 3u);
@@ -465,14 +470,14 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
   // tile is padded) so that no control flow separates a read from its use and
   // the waitcnt pass can count the in-order LDS returns instead of draining.
   float pc[3];
-  read3c(pc, row, off);
+  read3c<ST>(pc, row, off);
 #pragma unroll 1
   for (int k = 0; k < 16; ++k) {
     if (k < K) {
       const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
       const int offn = max(off - size1(idn), 0);
       float pn[3];
-      read3c(pn, row, offn);
+      read3c<ST>(pn, row, offn);
       l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
       id = idn;
       off = offn;
@@ -485,29 +490,30 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
 }
 
 // Base log-density at d = 1 (fast math), shared by every d = 1 evaluator.
+template <int ST = 1>
 __device__ __forceinline__ float base1_fast(float z, const float* row, bool trainable) {
   if (trainable) {
-    const float sc = 1e-3f + sp_fast1(kLogExpm1One + 0.1f * row[1]);
+    const float sc = 1e-3f + sp_fast1(kLogExpm1One + 0.1f * row[ST]);
     const float zz = f_div<true>(z - row[0], sc);
     return -0.5f * (zz * zz) - (kHalfLog2Pi + __builtin_amdgcn_logf(sc) * kLn2);
   }
   return -0.5f * (z * z) - kHalfLog2Pi;
 }
 
-template <bool PACKED>
+template <bool PACKED, int ST = 1>
 __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, const ChainArgs& a) {
   const int K = a.prog.K;
   float l2 = 0.0f;  // sum of log2|det J_k|
   if constexpr (PACKED) {
-    if (K > 0) l2 = chain1_fast_packed(z, row, a.prog.types[0], K, a.P);
+    if (K > 0) l2 = chain1_fast_packed<ST>(z, row, a.prog.types[0], K, a.P);
   } else if (K > 0) {
     int st = a.prog.step[0];
     float pc[3];
-    read3(pc, row, st);
+    read3<ST>(pc, row, st);
     for (int k = 0; k < K; ++k) {
       const int stn = (k + 1 < K) ? a.prog.step[k + 1] : 0;
       float pn[3];
-      if (k + 1 < K) read3(pn, row, stn);
+      if (k + 1 < K) read3<ST>(pn, row, stn);
       const int id = st & 3;
       float l;
       if (id == NFN_FLOW_PLANAR)
@@ -523,7 +529,7 @@ __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, con
       pc[2] = pn[2];
     }
   }
-  return base1_fast(z, row, a.trainable != 0) + l2 * kLn2;
+  return base1_fast<ST>(z, row, a.trainable != 0) + l2 * kLn2;
 }
 
 // One evaluator per (DM, FAST) for every kernel, so all tile-streaming strategies

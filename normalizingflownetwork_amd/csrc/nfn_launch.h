@@ -62,6 +62,11 @@ bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_
 bool launch_grad_group_fast(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s,
                                int64_t* grid);
+// chain_dense1_kernel's t tile: column-major at this padded column stride (floats),
+// overlaying the wave's h tile (dead once the A fragments are in registers): one
+// wave's LDS region in floats
+constexpr int kCS = 68;
+__host__ __device__ inline int dense1_wave_floats(int P, int SH) { return std::max(64 * SH, (P + 1) * kCS); }
 // nfn_dense.hip; false if (dm, H) has no instance
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
 // nfn_sample.hip
