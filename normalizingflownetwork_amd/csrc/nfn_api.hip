@@ -125,7 +125,7 @@ int group_lds_stride(int P, int G) {
 void group_shape(int dm, int want_g, int* G, int* DPL) {
   struct Shape { int dm, g, dpl; };
   static const Shape defaults[] = {{4, 4, 1}, {8, 4, 2}, {16, 4, 4}, {32, 8, 4}};
-  static const Shape alts[] = {{8, 8, 1}, {16, 8, 2}};
+  static const Shape alts[] = {{8, 8, 1}, {16, 8, 2}, {8, 2, 4}};
   for (const Shape& x : defaults)
     if (x.dm == dm) { *G = x.g; *DPL = x.dpl; }
   for (const Shape& x : alts)
@@ -212,9 +212,15 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   const int Q = P >> 2;
   const int mode = load_mode_env();
   int G = 4, DPL = 1;
-  group_shape(dm, env_int("NFN_GROUP_LANES", 0), &G, &DPL);
+  // The plain forward with fast math and contiguous rows (chain_group1_kernel) runs
+  // d in (4, 8] as 2 lanes x 4 dimensions per sample: half the per-sample scalar work
+  // of 4 x 2 (C3 compute 0.40 -> 0.29 ms, kernel 0.400 -> 0.395 ms, now HBM-bound),
+  // while the prefetch of its 32-row tiles still fits (<= 18 float4 per lane).
+  const bool two_lane = !posterior && use_fast_math() && dm == 8 && t_rowstride == P && (Q + 1) / 2 <= 18;
+  group_shape(dm, env_int("NFN_GROUP_LANES", two_lane ? 2 : 0), &G, &DPL);
   const int nv_group = (Q + G - 1) / G;  // float4 slots per lane: (64/G rows x Q) / 64
-  const bool group_ok = a.vec4 && t_rowstride != 0 && d >= 4 && Q >= 1 && nv_group <= 16 && mode != kTile &&
+  const bool group_ok = a.vec4 && t_rowstride != 0 && d >= 4 && Q >= 1 && nv_group <= (G == 2 ? 18 : 16) &&
+                        mode != kTile &&
                         mode != kCoop && mode != kOwnRow && mode != kWave && env_int("NFN_GROUP", 1) != 0;
   bool launched_group = false;
   if (group_ok) {

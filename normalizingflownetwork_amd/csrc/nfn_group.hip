@@ -52,6 +52,8 @@ bool launch_g_nv(int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t*
     launch_g<G, DPL, 12, POST>(a, lds, s, g);
   else if (nv <= 16)
     launch_g<G, DPL, 16, POST>(a, lds, s, g);
+  else if (G == 2 && nv <= 18)
+    launch_g<G, DPL, 18, POST>(a, lds, s, g);
   else
     return false;
   return true;
@@ -68,6 +70,7 @@ bool launch_g_shape(int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipS
   if constexpr (kFast && !POST) {
     if (G == 8 && DPL == 1) return launch_g_nv<8, 1, POST>(nv, a, lds, s, g);
     if (G == 8 && DPL == 2) return launch_g_nv<8, 2, POST>(nv, a, lds, s, g);
+    if (G == 2 && DPL == 4) return launch_g_nv<2, 4, POST>(nv, a, lds, s, g);  // NFN_GROUP_LANES=2
   }
   return false;
 }

@@ -245,6 +245,8 @@ def main():
         return
     if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
         v = [{"name": "group1", "env": {}}, {"name": "group", "env": {"NFN_GROUP1": 0}},
+             {"name": "g4x2", "env": {"NFN_GROUP_LANES": 4}},
+             {"name": "g4x2_compute_only", "env": {"NFN_GROUP_LANES": 4, "NFN_ABLATE_LOADS": 1}},
              {"name": "group1_wg4", "env": {"NFN_WG_PER_CU": 4}},
              {"name": "group1_wg3", "env": {"NFN_WG_PER_CU": 3}},
              {"name": "group1_noprio", "env": {"NFN_PRIO": 0}},
@@ -329,6 +331,8 @@ def main():
         return
     if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
         v = [{"name": "group1", "env": {}}, {"name": "group", "env": {"NFN_GROUP1": 0}},
+             {"name": "g4x2", "env": {"NFN_GROUP_LANES": 4}},
+             {"name": "g4x2_compute_only", "env": {"NFN_GROUP_LANES": 4, "NFN_ABLATE_LOADS": 1}},
              {"name": "group1_wg4", "env": {"NFN_WG_PER_CU": 4}},
              {"name": "group1_wg3", "env": {"NFN_WG_PER_CU": 3}},
              {"name": "group1_noprio", "env": {"NFN_PRIO": 0}},
