@@ -165,3 +165,36 @@ def test_grad_full_size_c2_sampled(gpu):
     gt64, dt32, gy64, dy32 = _grads_ref(ys, ts, ft, d, True)
     _check(gt[idx].cpu().numpy(), gt64, dt32, "C2 sampled d/dt")
     _check(gy[idx].cpu().numpy(), gy64, dy32, "C2 sampled d/dy")
+
+
+def test_grad_c3_full_size_sampled_and_broadcast(gpu):
+    """C3 (d = 8, affine + planar x4 + radial x4) at full size with a ragged batch
+    (2^22 - 5: the last 16-row wave tile is partial) and an upstream gradient:
+    every gradient finite where log_prob is, sampled rows and the last rows against
+    the oracle; then y broadcast over the batch (batch stride 0) at d = 8."""
+    from normalizingflownetwork_amd import ops
+    from oracle import nfn_oracle as O
+
+    ft, d = ("affine",) + ("planar",) * 4 + ("radial",) * 4, 8
+    P = O.total_param_size(ft, d, True)
+    B = (1 << 22) - 5
+    gen = torch.Generator(device=gpu).manual_seed(23)
+    y = torch.randn((B, d), generator=gen, device=gpu)
+    t = torch.randn((B, P), generator=gen, device=gpu)
+    g = torch.randn((B,), generator=gen, device=gpu)
+    lp, gt, gy = ops.chain_log_prob_grad(y, t, ft, d, True, g_out=g, want_logp=True)
+    fin = torch.isfinite(lp)
+    assert torch.isfinite(gt[fin]).all() and torch.isfinite(gy[fin]).all()
+    idx = torch.cat([torch.randperm(B, generator=torch.Generator().manual_seed(3))[:1024],
+                     torch.arange(B - 40, B)]).to(gpu)
+    ys, ts, gs = y[idx].cpu().numpy(), t[idx].cpu().numpy(), g[idx].cpu().numpy()
+    gt64, dt32, gy64, dy32 = _grads_ref(ys, ts, ft, d, True, g=gs)
+    _check(gt[idx].cpu().numpy(), gt64, dt32, "C3 sampled d/dt")
+    _check(gy[idx].cpu().numpy(), gy64, dy32, "C3 sampled d/dy")
+    rng = np.random.default_rng(4)
+    y1 = rng.standard_normal((1, d)).astype(np.float32)
+    tb = rng.standard_normal((333, P)).astype(np.float32)
+    gt64, dt32, gy64, dy32 = _grads_ref(y1, tb, ft, d, True)
+    _, gtb, gyb = _run(gpu, y1, tb, ft, d, True)
+    _check(gtb, gt64, dt32, "C3 y-broadcast d/dt")
+    _check(gyb, gy64, dy32, "C3 y-broadcast d/dy")

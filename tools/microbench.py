@@ -211,10 +211,13 @@ def main():
         return
     if which[0] == "gradc3":  # C3 backward occupancy: waves per workgroup x register cap
         run_grad("C3", [{"name": "wpb4", "env": {}},
+                        {"name": "generic_walk", "env": {"NFN_GRAD_GROUP1": 0}},
                         {"name": "wpb2", "env": {"NFN_GRAD_GROUP_WPB": 2}},
+                        {"name": "wg_cap3", "env": {"NFN_WG_PER_CU": 3}},
                         {"name": "wpb2_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
                         {"name": "wpb2_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
-                        {"name": "wpb4_b", "env": {}}, {"name": "wpb2_b", "env": {"NFN_GRAD_GROUP_WPB": 2}}])
+                        {"name": "wpb4_b", "env": {}}, {"name": "generic_walk_b", "env": {"NFN_GRAD_GROUP1": 0}},
+                        {"name": "wpb2_b", "env": {"NFN_GRAD_GROUP_WPB": 2}}])
         return
     if which[0] == "grad":
         v = [{"name": "wave", "env": {}},
