@@ -226,6 +226,25 @@ int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t,
                               double* workspace, void* stream);
 
 /*
+ * Bayesian posterior score with the output DenseVariational layer fused
+ * (BayesianNNEstimator.py:65-76 score, :136-145 the variational output layer):
+ *   out_lse[b] = logsumexp_s( logp(y_b | t_sb = h_sb W_s + bias_s) [- sum log y_std] ) - log(S)
+ * with t_sb formed on chip (fp32 MFMA), never written to memory.
+ *   h    : draw s, sample b at h + s*h_drawstride + b*h_rowstride (h_drawstride 0 = one h
+ *          shared by every draw); H in {4, 8, 16, 32, 64}; 16-byte aligned, strides multiples of 4
+ *   W    : draw s at W + s*w_drawstride, (H, P) row-major;  bias : draw s at
+ *          bias + s*bias_drawstride, (P,), or NULL
+ *   P <= 64, d <= 8 (else NFN_E_SHAPE).  out_sum / workspace as for nfn_chain_logprob_f32
+ *   (nfn_chain_workspace_doubles).
+ */
+int32_t nfn_posterior_lse_dense_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_drawstride,
+                                    int64_t h_rowstride, int32_t H, const float* W, int64_t w_drawstride,
+                                    const float* bias, int64_t bias_drawstride, int32_t S, int64_t B, int32_t d,
+                                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                                    const float* y_std, float* out_lse, double* out_sum, double* workspace,
+                                    void* stream);
+
+/*
  * Multi-GPU (one process per GPU, batch sharded over ranks).  The communicator
  * is RCCL over xGMI; its handle is opaque (`void*` = ncclComm_t).
  *   nfn_comm_unique_id : rank 0 creates the 128-byte rendezvous id, which the

@@ -53,6 +53,11 @@ SIGNATURES = {
         [_vp, _c_int64, _vp, _c_int64, _c_int32, _vp, _vp, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp,
          _vp, _vp, _vp, _vp],
     ),
+    "nfn_posterior_lse_dense_f32": (
+        _c_int32,
+        [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int64, _vp, _c_int64, _c_int32, _c_int64,
+         _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp, _vp, _vp, _vp],
+    ),
     "nfn_chain_sample_f32": (
         _c_int32,
         [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp, _vp, _vp, _vp],

@@ -441,6 +441,73 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   return rc;
 }
 
+int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_drawstride,
+                            int64_t h_rowstride, int32_t H, const float* W, int64_t w_drawstride, const float* bias,
+                            int64_t b_drawstride, int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
+                            int32_t trainable_base, const float* y_mean, const float* y_std, float* out,
+                            double* out_sum, double* workspace, void* stream) {
+  g_last_error.clear();
+  DenseArgs da;
+  memset(&da, 0, sizeof(da));
+  ChainArgs& a = da.c;
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMMs + streaming alone
+  if (P < 0) return P;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
+  if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");
+  if (H < 4 || H > 64 || (H & (H - 1)) != 0) return fail(NFN_E_SHAPE, "hidden width H must be 4, 8, 16, 32 or 64");
+  if (P < 1 || P > 64) return fail(NFN_E_SHAPE, "fused dense path needs 1 <= P <= 64");
+  if (d > 8) return fail(NFN_E_SHAPE, "fused dense path needs n_dims <= 8");
+  if (h_rowstride < H || (h_rowstride & 3) != 0) return fail(NFN_E_SHAPE, "h row stride must be >= H and a multiple of 4");
+  if (h_drawstride < 0 || (h_drawstride & 3) != 0 || (h_drawstride != 0 && h_drawstride < B * h_rowstride))
+    return fail(NFN_E_SHAPE, "h draw stride must be 0 (shared h) or >= B * h_rowstride, a multiple of 4");
+  if (w_drawstride < 0 || (S > 1 && w_drawstride < (int64_t)H * P)) return fail(NFN_E_SHAPE, "W draw stride < H * P");
+  if (bias && (b_drawstride < 0 || (S > 1 && b_drawstride < P))) return fail(NFN_E_SHAPE, "bias draw stride < P");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B == 0) {
+    if (out_sum && hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+    return NFN_OK;
+  }
+  if (!y || !h || !W) return fail(NFN_E_NULLPTR, "y, h or W is NULL");
+  if ((reinterpret_cast<uintptr_t>(h) & 15) != 0) return fail(NFN_E_SHAPE, "h must be 16-byte aligned");
+  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
+  if (!out && !workspace) return NFN_OK;
+  a.y = y;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.out = out;
+  a.partials = workspace ? workspace + 1 : nullptr;
+  a.y_bstride = y_bstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = P | 1;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = S;
+  a.ntiles = (B + 63) / 64;
+  da.h = h;
+  da.h_rowstride = h_rowstride;
+  da.h_drawstride = h_drawstride;
+  da.W = W;
+  da.w_drawstride = w_drawstride;
+  da.bias = bias;
+  da.b_drawstride = b_drawstride;
+  da.H = H;
+  da.h_lds_stride = H | 1;
+  int64_t grid = 0;
+  if (!launch_posterior_dense(use_fast_math(), dm_for(d), da, s, &grid))
+    return fail(NFN_E_SHAPE, "no fused dense posterior instance for this shape");
+  int32_t rc = check_hip("posterior_dense_kernel launch");
+  if (rc != NFN_OK) return rc;
+  if (out_sum) {
+    launch_reduce_partials((const double*)workspace, out_sum, s);
+    rc = check_hip("reduce_partials_kernel launch");
+  }
+  return rc;
+}
+
 int32_t run_sample(const float* eps, int64_t eps_bstride, const float* t, int64_t t_rowstride, int64_t B, int32_t d,
                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                    const float* y_std, float* y_out, float* logp_out, void* stream) {
@@ -620,6 +687,16 @@ int32_t nfn_chain_logprob_dense_f32(const float* y, int64_t y_bstride, const flo
                                     void* stream) {
   return run_dense(y, y_bstride, h, h_rowstride, H, W, bias, B, d, flow_ids, K, trainable_base, y_mean, y_std,
                    out_logp, out_sum, workspace, stream);
+}
+
+int32_t nfn_posterior_lse_dense_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_drawstride,
+                                    int64_t h_rowstride, int32_t H, const float* W, int64_t w_drawstride,
+                                    const float* bias, int64_t bias_drawstride, int32_t S, int64_t B, int32_t d,
+                                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
+                                    const float* y_std, float* out_lse, double* out_sum, double* workspace,
+                                    void* stream) {
+  return run_posterior_dense(y, y_bstride, h, h_drawstride, h_rowstride, H, W, w_drawstride, bias, bias_drawstride, S,
+                             B, d, flow_ids, K, trainable_base, y_mean, y_std, out_lse, out_sum, workspace, stream);
 }
 
 int32_t nfn_chain_sample_f32(const float* eps, int64_t eps_bstride, const float* t, int64_t t_rowstride, int64_t B,

@@ -282,6 +282,295 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   }
 }
 
+// Bayesian posterior with the output DenseVariational layer fused
+// (BayesianNNEstimator.py:65-76 score over draws, :136-145 the variational output
+// layer): per sample, logsumexp over S draws of log_prob(y | t_s = h_s W_s + b_s) - log S.
+// d = 1, fast math.  A wave walks (tile, draw) units — its 64-sample tile through all
+// S draws — with chain_dense1_kernel's memory pipeline: the NEXT unit's h tile, y and
+// W / bias fragments are prefetched (buffer loads, counted waits) while the current
+// unit runs the MFMA GEMM and the chain; the tile's result leaves once, after its
+// last draw (the per-unit store of the other draws goes through an empty descriptor).
+template <int QH, int NN>
+__global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs da) {
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  constexpr int RSTEP = 64 / QH;
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int SH = da.h_lds_stride;
+  const int P = a.P;
+  const int S = a.S;
+  float* hl = lds + wid * dense1_wave_floats(P, SH);
+  float* tl = hl;
+  const int r0 = lane / QH, c4 = lane % QH;
+  const int l0 = r0 * SH + 4 * c4;
+  const int am = lane & 15, ak = lane >> 4;
+  const int64_t hs = da.h_rowstride;
+  const int64_t ntiles = a.ntiles;
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int hoff = (r0 * (int)hs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)hs * 4;
+  int woff[QH][NN];  // this lane's B-fragment offsets in W_s (bytes); columns >= P read row 0 and are zeroed
+  bool wcol[NN];
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    wcol[nt] = 16 * nt + am < P;
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks) woff[ks][nt] = wcol[nt] ? ((4 * ks + ak) * P + 16 * nt + am) * 4 : 0;
+  }
+  float4 buf[QH];
+  float ybuf;
+  float wbuf[QH][NN], bbuf[NN];
+  auto issue = [&](int64_t tile, int sd) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const auto rh = tile_rsrc(da.h + sd * da.h_drawstride + b0c * hs, nr > 0 ? ((nr - 1) * hs + 4 * QH) * 4 : 0);
+#pragma unroll
+    for (int k = 0; k < QH; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, k * kstep, kNT));
+    const auto rw = tile_rsrc(da.W + sd * da.w_drawstride, nr > 0 ? (int64_t)4 * QH * P * 4 : 0);
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt)
+        wbuf[ks][nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, woff[ks][nt], 0, 0));
+    const auto rb = tile_rsrc(da.bias ? da.bias + sd * da.b_drawstride : da.W, (da.bias && nr > 0) ? P * 4 : 0);
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt)
+      bbuf[nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (16 * nt + am) * 4, 0, 0));
+  };
+  double acc_sum = 0.0;
+  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
+  float pend_v = 0.0f;
+  auto flush = [&]() {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  };
+  issue(u0, 0);
+  flush();  // empty: every path into the loop ends [loads][store]
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    float m = -INFINITY, lacc = 0.0f;
+    for (int sd = 0; sd < S; ++sd) {
+#pragma unroll
+      for (int k = 0; k < QH; ++k) {
+        float* dst = hl + l0 + k * RSTEP * SH;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
+      float wv[QH][NN], bv[NN];
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt) {
+        bv[nt] = bbuf[nt];
+#pragma unroll
+        for (int ks = 0; ks < QH; ++ks) wv[ks][nt] = wcol[nt] ? wbuf[ks][nt] : 0.0f;
+      }
+      const float z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+      wave_lds_sync();
+      const bool last = sd + 1 == S;
+      issue(last ? tile + ustep : tile, last ? 0 : sd + 1);
+      flush();
+      pend_r = tile_rsrc(a.out, 0);  // later draws of this tile store nothing
+      float av[4][QH];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < QH; ++ks) av[mt][ks] = hl[(16 * mt + am) * SH + 4 * ks + ak];
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt) {
+        f32x4v acc[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][ks], wv[ks][nt], acc[mt], 0, 0, 0);
+        const int n = 16 * nt + am;
+        if (n < P) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            *reinterpret_cast<f32x4v*>(tl + n * kCS + 16 * mt + 4 * ak) = acc[mt] + bv[nt];
+        }
+      }
+      wave_lds_sync();
+      const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS>(z0, tl + lane, a)
+                                       : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
+      lse_push<true>(m, lacc, lp);
+      wave_lds_sync();  // this unit's LDS reads done before the next unit's writes
+    }
+    const float res = lse_finish<true>(m, lacc, S);
+    if (lane < nr) acc_sum += (double)res;
+    pend_v = res;
+    pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+  }
+  flush();
+  if (a.partials) {
+    const double sum = block_sum(acc_sum, red);
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
+
+// The posterior for any d <= 8 and either math mode: one tile of 64 samples per
+// wave, the S draws in turn (h_s rows staged to LDS, W_s fragments read from
+// global memory / L2, t_s = h_s W_s + b_s on the matrix cores, the chain, the
+// online logsumexp).  Plain synchronous loads: the generality path.
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock) posterior_dense_kernel(DenseArgs da) {
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  __shared__ double red[kMaxBlock / 64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int H = da.H;
+  const int QH = H >> 2;
+  const int SH = da.h_lds_stride;
+  const int S = a.lds_stride;
+  const int P = a.P;
+  const int NN = (P + 15) >> 4;
+  float* hl = lds + wid * (64 * SH + 64 * S);
+  float* tl = hl + 64 * SH;
+  const int am = lane & 15, ak = lane >> 4;
+  const int64_t hs = da.h_rowstride;
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  float corr = 0.0f;
+  if (a.y_mean) {
+    for (int j = 0; j < a.d; ++j) corr += f_log<FAST>(a.y_std[j]);
+  }
+  double acc_sum = 0.0;
+  for (int64_t tile = u0; tile < a.ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int nr = (int)min((int64_t)64, a.B - b0);
+    float z0[DM];
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+      z0[j] = (lane < nr && j < a.d) ? a.y[(b0 + lane) * a.y_bstride + j] : 0.0f;
+      if (a.y_mean && j < a.d) z0[j] = f_div<FAST>(z0[j] - a.y_mean[j], a.y_std[j]);
+    }
+    float m = -INFINITY, lacc = 0.0f;
+    for (int sd = 0; sd < a.S; ++sd) {
+      const float* hsrc = da.h + sd * da.h_drawstride + b0 * hs;
+      for (int i = lane; i < 64 * QH; i += 64) {
+        const int r = i / QH, c = i - (i / QH) * QH;
+        const float4 v = r < nr ? load_row4<true>(hsrc + (int64_t)r * hs + 4 * c) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float* dst = hl + r * SH + 4 * c;
+        dst[0] = v.x;
+        dst[1] = v.y;
+        dst[2] = v.z;
+        dst[3] = v.w;
+      }
+      wave_lds_sync();
+      const float* Ws = da.W + sd * da.w_drawstride;
+      for (int nt = 0; nt < NN; ++nt) {
+        const int n = 16 * nt + am;
+        f32x4v acc[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int ks = 0; ks < QH; ++ks) {
+          const float bv = n < P ? Ws[(4 * ks + ak) * P + n] : 0.0f;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            const float av = hl[(16 * mt + am) * SH + 4 * ks + ak];
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mt], 0, 0, 0);
+          }
+        }
+        if (n < P) {
+          const float bn = da.bias ? da.bias[sd * da.b_drawstride + n] : 0.0f;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tl[(16 * mt + 4 * ak + i) * S + n] = acc[mt][i] + bn;
+          }
+        }
+      }
+      wave_lds_sync();
+      float z[DM];
+#pragma unroll
+      for (int j = 0; j < DM; ++j) z[j] = z0[j];
+      const float lp = eval_chain<DM, FAST>(z, tl + lane * S, a) - corr;
+      lse_push<FAST>(m, lacc, lp);
+      wave_lds_sync();
+    }
+    if (lane < nr) {
+      const float res = lse_finish<FAST>(m, lacc, a.S);
+      if (a.out) __builtin_nontemporal_store(res, a.out + b0 + lane);
+      acc_sum += (double)res;
+    }
+  }
+  if (a.partials) {
+    const double sum = block_sum(acc_sum, red);
+    if (tid == 0) {
+      a.partials[blockIdx.x] = sum;
+      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
+    }
+  }
+}
+
+template <int QH>
+void launch_pd1(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
+  const int nn = (da.c.P + 15) >> 4;
+  const size_t lds = (size_t)(4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
+  auto kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1>
+                     : (nn == 2 ? posterior_dense1_kernel<QH, 2> : (nn == 3 ? posterior_dense1_kernel<QH, 3>
+                                                                            : posterior_dense1_kernel<QH, 4>));
+  int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+}
+
+template <int DM, bool FAST>
+void launch_pd(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
+  auto kfn = posterior_dense_kernel<DM, FAST>;
+  const size_t lds = (size_t)(4 * (64 * da.h_lds_stride + 64 * da.c.lds_stride) + 16) * sizeof(float);
+  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+}
+
+template <bool FAST>
+bool launch_pd_dm(int dm, const DenseArgs& da, hipStream_t s, int64_t* g) {
+  const ChainArgs& a = da.c;
+  if constexpr (FAST) {
+    if (dm == 1 && a.d == 1 && env_int("NFN_DENSE1", 1) != 0 && da.h_rowstride * 256 < ((int64_t)1 << 31) &&
+        a.y_bstride * 256 < ((int64_t)1 << 31)) {
+      switch (da.H >> 2) {
+        case 1: launch_pd1<1>(da, s, g); return true;
+        case 2: launch_pd1<2>(da, s, g); return true;
+        case 4: launch_pd1<4>(da, s, g); return true;
+        case 8: launch_pd1<8>(da, s, g); return true;
+      }
+    }
+  }
+  switch (dm) {
+    case 1: launch_pd<1, FAST>(da, s, g); return true;
+    case 2: launch_pd<2, FAST>(da, s, g); return true;
+    case 4: launch_pd<4, FAST>(da, s, g); return true;
+    case 8: launch_pd<8, FAST>(da, s, g); return true;
+  }
+  return false;
+}
+
 template <int QH>
 void launch_d1(const DenseArgs& da, size_t /*generic kernel's LDS*/, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
@@ -341,6 +630,10 @@ bool launch_d_dm(int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s
 
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid) {
   return fast ? launch_d_dm<true>(dm, nvh, da, lds, s, grid) : launch_d_dm<false>(dm, nvh, da, lds, s, grid);
+}
+
+bool launch_posterior_dense(bool fast, int dm, const DenseArgs& da, hipStream_t s, int64_t* grid) {
+  return fast ? launch_pd_dm<true>(dm, da, s, grid) : launch_pd_dm<false>(dm, da, s, grid);
 }
 
 }  // namespace nfn

@@ -108,6 +108,11 @@ struct DenseArgs {
   const float* bias;     // (P,) or NULL
   int32_t H;
   int32_t h_lds_stride;  // odd, > H
+  // posterior (c.S draws): draw s uses h + s*h_drawstride (0 = shared h),
+  // W + s*w_drawstride and bias + s*b_drawstride
+  int64_t h_drawstride;
+  int64_t w_drawstride;
+  int64_t b_drawstride;
 };
 
 // Sampling through the inverted flows (nfn_sample.hip).

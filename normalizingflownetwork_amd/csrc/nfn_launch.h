@@ -69,6 +69,7 @@ constexpr int kCS = 68;
 __host__ __device__ inline int dense1_wave_floats(int P, int SH) { return std::max(64 * SH, (P + 1) * kCS); }
 // nfn_dense.hip; false if (dm, H) has no instance
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
+bool launch_posterior_dense(bool fast, int dm, const DenseArgs& da, hipStream_t s, int64_t* grid);
 // nfn_sample.hip
 void launch_sample(bool fast, int dm, const SampleArgs& sa, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_grid.hip

@@ -276,6 +276,67 @@ def chain_log_prob_dense(
     return out, osum
 
 
+def posterior_lse_dense(
+    y,
+    h,
+    W,
+    b,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+    want_values: bool = True,
+    want_sum: bool = False,
+):
+    """Bayesian posterior score per sample with the output DenseVariational layer fused
+    (``BayesianNNEstimator.py:65-76`` score over draws, ``:136-145`` the variational output
+    layer): ``logsumexp_s log_prob(y | h_s W_s + b_s) - log S``.  ``h``: (S, B, H) per-draw
+    last hidden activations, or (B, H) shared by every draw; ``W``: (S, H, P); ``b``: (S, P)
+    or None.  Shapes the fused kernel does not take run as a library GEMM (torch) followed
+    by :func:`posterior_lse`."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    h = as_device_f32(h, dev)
+    W = as_device_f32(W, dev).contiguous()
+    assert W.dim() == 3 and W.shape[2] == P, f"W must be (S, H, {P})"
+    S, H = int(W.shape[0]), int(W.shape[1])
+    assert h.dim() in (2, 3) and h.shape[-1] == H, f"h must be (S, B, {H}) or (B, {H})"
+    if h.dim() == 3:
+        assert h.shape[0] == S, "h and W disagree on the number of draws"
+    bb = None
+    if b is not None:
+        bb = as_device_f32(b, dev).reshape(S, P).contiguous()
+    B = int(h.shape[-2])
+    hrow = int(h.stride(-2))
+    hdraw = int(h.stride(0)) if h.dim() == 3 else 0
+    aligned = h.stride(-1) == 1 and hrow % 4 == 0 and hdraw % 4 == 0 and h.data_ptr() % 16 == 0
+    if h.dim() == 3 and S > 1 and hdraw < B * hrow:
+        aligned = False
+    if not dense_fusable(H, P, n_dims) or not aligned:
+        hd = h if h.dim() == 3 else h.unsqueeze(0).expand(S, B, H)
+        t = torch.matmul(hd, W) + (bb.unsqueeze(1) if bb is not None else 0.0)
+        return posterior_lse(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, want_values, want_sum)
+    y = _prep_2d(y, n_dims, "y", dev)
+    assert y.shape[0] in (1, B), "incompatible batch sizes"
+    ym = ys = None
+    if y_mean is not None:
+        ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+        ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
+    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    lib = _lib.load()
+    ws = _workspace(int(lib.nfn_chain_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
+    ids, k = flow_ids(flow_types)
+    rc = lib.nfn_posterior_lse_dense_f32(
+        _ptr(y), _row_stride(y), _ptr(h), hdraw, hrow, H, _ptr(W), H * P, _ptr(bb), P, S, B, int(n_dims),
+        ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys), _ptr(out), _ptr(osum),
+        _ptr(ws), _stream(),
+    )
+    _lib.check(rc, "nfn_posterior_lse_dense_f32")
+    return out, osum
+
+
 class DenseLauncher:
     """Pre-bound fused Dense->chain launch over fixed device buffers (benchmark loop)."""
 

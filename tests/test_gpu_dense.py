@@ -67,3 +67,89 @@ def test_dense_with_normalisation_and_fallback(gpu):
         ref64 = O.log_pdf(y, t64, ft, d, True, ym, ys, np.float64)
         ref32 = O.log_pdf(y, t32, ft, d, True, ym, ys, np.float32)
         assert np.all(np.abs(out.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32)), H
+
+
+def _post_case(ft, d, H, B, S, seed, shared_h=False, bias=True):
+    rng = np.random.default_rng(seed)
+    P = O.total_param_size(ft, d, True)
+    h = rng.standard_normal((B, H) if shared_h else (S, B, H)).astype(np.float32)
+    W = (rng.standard_normal((S, H, P)) / np.sqrt(H)).astype(np.float32)
+    b = (0.1 * rng.standard_normal((S, P))).astype(np.float32) if bias else None
+    y = rng.standard_normal((B, d)).astype(np.float32)
+    hd = np.broadcast_to(h, (S, B, H)) if shared_h else h
+    t64 = np.matmul(hd.astype(np.float64), W.astype(np.float64)) + (0 if b is None else b.astype(np.float64)[:, None])
+    t32 = (np.matmul(hd, W) + (0 if b is None else b[:, None])).astype(np.float32)
+    return h, W, b, y, t64, t32
+
+
+@pytest.mark.parametrize("ft,d,H,B,S,shared", [
+    (("planar", "radial") * 5, 1, 16, 1000, 8, False),   # the C5 chain (fused d = 1 kernel)
+    (("planar", "radial") * 5, 1, 16, 777, 5, True),     # h shared by every draw (h draw stride 0)
+    (("radial", "radial"), 1, 4, 333, 3, False),
+    (("radial",) * 14, 1, 8, 301, 2, False),             # P = 44: three 16-column N tiles
+    (("affine", "planar", "radial"), 3, 8, 300, 4, False),  # generic posterior kernel (d > 1)
+    (("planar", "affine"), 8, 16, 129, 3, True),
+    (("planar", "radial") * 2, 1, 32, 65, 1, False),     # S = 1
+])
+def test_posterior_dense_matches_oracle(math_mode, ft, d, H, B, S, shared):
+    """Bayesian posterior score with the output DenseVariational layer fused
+    (BayesianNNEstimator.py:65-76, :136-145): against the oracle's posterior_lse on
+    t_s = h_s W_s + b_s computed in fp64 (truth) / fp32 (the conditioning bound)."""
+    from normalizingflownetwork_amd import ops
+
+    h, W, b, y, t64, t32 = _post_case(ft, d, H, B, S, seed=H + B + S, shared_h=shared)
+    out, s = ops.posterior_lse_dense(torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(),
+                                     torch.from_numpy(W).cuda(), torch.from_numpy(b).cuda(), ft, d, True,
+                                     want_sum=True)
+    ref64 = O.posterior_lse(y, t64, ft, d, True, dtype=np.float64)
+    ref32 = O.posterior_lse(y, t32, ft, d, True, dtype=np.float32)
+    got = out.cpu().numpy()
+    ok = np.isfinite(ref64)
+    bound = O.tolerance_bound(ref64, ref32)
+    bad = ok & ~(np.abs(got - ref64) <= bound)
+    assert not bad.any(), (int(bad.sum()), got[bad][:4], ref64[bad][:4])
+    assert abs(s.item() - ref64[ok].sum()) <= bound[ok].sum() + 1e-6 * abs(ref64[ok].sum()) or not ok.all()
+
+
+def test_posterior_dense_normalised_nobias_and_fallback(gpu):
+    """y normalisation fused, no bias, and the unsupported-shape fallback (H = 12:
+    library GEMM + posterior kernel) — all against the oracle."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d, S = ("planar", "radial") * 3, 1, 4
+    ym, ys = np.array([0.3], np.float32), np.array([1.4], np.float32)
+    for H, bias in ((16, False), (12, True)):
+        h, W, b, y, t64, t32 = _post_case(ft, d, H, 257, S, seed=7 + H, bias=bias)
+        bb = None if b is None else torch.from_numpy(b).cuda()
+        out, _ = ops.posterior_lse_dense(torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(),
+                                         torch.from_numpy(W).cuda(), bb, ft, d, True, ym, ys)
+        ref64 = O.posterior_lse(y, t64, ft, d, True, ym, ys, np.float64)
+        ref32 = O.posterior_lse(y, t32, ft, d, True, ym, ys, np.float32)
+        assert np.all(np.abs(out.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32)), H
+
+
+def test_posterior_dense_full_size_c5_sampled(gpu):
+    """C5 per-GPU shape (S = 64 draws x B = 2^17, H = 16): the fused kernel equals the
+    unfused path (t_s materialised by the library GEMM, then the posterior kernel)
+    within the fp32 GEMM-rounding bound, and sampled rows match the oracle."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d, S, B, H = ("planar", "radial") * 5, 1, 64, 1 << 17, 16
+    P = O.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    h = torch.randn((S, B, H), generator=gen, device="cuda")
+    W = torch.randn((S, H, P), generator=gen, device="cuda") / 4.0
+    b = 0.1 * torch.randn((S, P), generator=gen, device="cuda")
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    out, s = ops.posterior_lse_dense(y, h, W, b, ft, d, True, want_sum=True)
+    assert torch.isfinite(out).all()
+    idx = torch.randperm(B, generator=torch.Generator().manual_seed(2))[:256]
+    hs, Ws, bs = h[:, idx.cuda()].cpu().numpy(), W.cpu().numpy(), b.cpu().numpy()
+    t64 = np.matmul(hs.astype(np.float64), Ws.astype(np.float64)) + bs.astype(np.float64)[:, None]
+    t32 = (np.matmul(hs, Ws) + bs[:, None]).astype(np.float32)
+    ys = y[idx.cuda()].cpu().numpy()
+    ref64 = O.posterior_lse(ys, t64, ft, d, True, dtype=np.float64)
+    ref32 = O.posterior_lse(ys, t32, ft, d, True, dtype=np.float32)
+    got = out[idx.cuda()].cpu().numpy()
+    assert np.all(np.abs(got - ref64) <= O.tolerance_bound(ref64, ref32))
+    assert abs(s.item() - out.double().sum().item()) <= 1e-9 * abs(s.item()) + 1e-6

@@ -169,8 +169,54 @@ def run_dense(variants, H=16, reps=20, rounds=3):
                           "rounds_ms": times[v["name"]]}), flush=True)
 
 
+def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
+    """C5 per-GPU shape with the output DenseVariational layer: fused posterior
+    (t_s formed on chip) vs the unfused path (library GEMM writes t, then the
+    posterior kernel) vs the posterior kernel alone on a resident t."""
+    ft, d = ("planar", "radial") * 5, 1
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    h = torch.randn((S, B, H), generator=gen, device="cuda")
+    W = torch.randn((S, H, P), generator=gen, device="cuda") / float(np.sqrt(H))
+    b = 0.1 * torch.randn((S, P), generator=gen, device="cuda")
+    t = torch.matmul(h, W) + b[:, None]
+    fns = {
+        "fused": lambda: ops.posterior_lse_dense(y, h, W, b, ft, d, True),
+        "unfused_gemm_plus_posterior": lambda: ops.posterior_lse(y, torch.matmul(h, W) + b[:, None], ft, d, True),
+        "posterior_on_resident_t": lambda: ops.posterior_lse(y, t, ft, d, True),
+    }
+    stream = torch.cuda.current_stream()
+    prewarm(fns["fused"])
+    times = {k: [] for k in fns}
+    outs = {}
+    for r in range(rounds):
+        for k, fn in fns.items():
+            for _ in range(3):
+                fn()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in evs:
+                e0.record(stream)
+                fn()
+                e1.record(stream)
+            torch.cuda.synchronize()
+            times[k].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+            if r == 0:
+                outs[k] = fn()[0].clone()
+    ref = outs["unfused_gemm_plus_posterior"]
+    for k in fns:
+        ms = float(np.median(times[k]))
+        print(json.dumps({"cfg": "C5", "mode": "posterior_dense", "H": H, "S": S, "B": B, "variant": k, "ms": ms,
+                          "pairs_per_s": S * B / ms * 1e3,
+                          "maxdiff_vs_unfused": float((outs[k] - ref).abs().max().item()),
+                          "rounds_ms": times[k]}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "pdense":
+        run_posterior_dense()
+        return
     if which[0] == "ceiling":  # HBM ceilings of plain torch streams over the C2 parameter buffer
         B, P = 1 << 24, 32
         t = torch.randn((B, P), device="cuda")
