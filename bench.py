@@ -100,14 +100,20 @@ def cpu_baseline_dense(cfg: str, H: int, seconds: float = 12.0, sample_rows: int
     as Keras' Dense) followed by the op-by-op chain restatement, 1 thread."""
     from oracle import nfn_oracle as O
 
-    ft, d, _, _ = CONFIGS[cfg]
+    ft, d, _, S = CONFIGS[cfg]
     P = O.total_param_size(ft, d, True)
     rng = np.random.default_rng(22)
-    y = rng.standard_normal((sample_rows, d)).astype(np.float32)
-    h = rng.standard_normal((sample_rows, H)).astype(np.float32)
-    W = (rng.standard_normal((H, P)) / np.sqrt(H)).astype(np.float32)
-    b = (0.1 * rng.standard_normal(P)).astype(np.float32)
-    run = lambda: O.chain_log_prob(y, h @ W + b, ft, d, True, np.float32)  # noqa: E731
+    rows = sample_rows if S is None else max(1, sample_rows // S)
+    lead = () if S is None else (S,)
+    y = rng.standard_normal((rows, d)).astype(np.float32)
+    h = rng.standard_normal(lead + (rows, H)).astype(np.float32)
+    W = (rng.standard_normal(lead + (H, P)) / np.sqrt(H)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(lead + (P,))).astype(np.float32)
+    if S is None:
+        run = lambda: O.chain_log_prob(y, h @ W + b, ft, d, True, np.float32)  # noqa: E731
+    else:  # the posterior over S draws of the output DenseVariational layer
+        run = lambda: O.posterior_lse(y, np.matmul(h, W) + b[:, None], ft, d, True, dtype=np.float32)  # noqa: E731
+    sample_rows = rows * (1 if S is None else S)
     from threadpoolctl import threadpool_limits
 
     with threadpool_limits(limits=1):  # one BLAS thread: the baseline is single-core
@@ -120,7 +126,7 @@ def cpu_baseline_dense(cfg: str, H: int, seconds: float = 12.0, sample_rows: int
             if el >= seconds or reps >= 50:
                 break
     return {"value": reps * sample_rows / el, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": f"{sample_rows} samples of {cfg} with H={H}: numpy fp32 GEMM + op-by-op chain "
+            "sample": f"{sample_rows} {'samples' if S is None else '(draw, sample) pairs'} of {cfg} with H={H}: numpy fp32 GEMM + op-by-op chain "
                       f"(oracle/nfn_oracle.py), {reps} reps in {el:.1f}s"}
 
 
@@ -221,14 +227,15 @@ def main():
     grad_mode = args.mode == "grad"
     dense_mode = args.mode == "dense"
     if dense_mode:
-        assert S is None, "--mode dense covers the plain chain configs"
+        # C5: the posterior with the output DenseVariational layer fused (per draw h_s, W_s, b_s)
         H = args.hidden
         del t
         hgen = torch.Generator(device=dev).manual_seed(122 + rank)
-        h = torch.randn((B, H), generator=hgen, device=dev)
-        Wd = torch.randn((H, P), generator=hgen, device=dev) / float(np.sqrt(H))
-        bd = 0.1 * torch.randn((P,), generator=hgen, device=dev)
-        launcher = ops.DenseLauncher(y, h, Wd, bd, ft, d, True)
+        lead = () if S is None else (S,)
+        h = torch.randn(lead + (B, H), generator=hgen, device=dev)
+        Wd = torch.randn(lead + (H, P), generator=hgen, device=dev) / float(np.sqrt(H))
+        bd = 0.1 * torch.randn(lead + (P,), generator=hgen, device=dev)
+        launcher = (ops.DenseLauncher if S is None else ops.PosteriorDenseLauncher)(y, h, Wd, bd, ft, d, True)
     elif grad_mode:
         assert S is None, "--mode grad covers the plain chain configs (C2, C3)"
         g_up = torch.full((B,), -1.0 / B, dtype=torch.float32, device=dev)  # d(mean NLL)/d log_prob
@@ -338,15 +345,22 @@ def main():
     if dense_mode and rank == 0:
         # the same x->density work unfused: t = h W + b by the library GEMM (t written to
         # HBM), then the chain kernel over t (read back) — what the fusion replaces
-        t_buf = torch.empty((B, P), dtype=torch.float32, device=dev)
-        plain = ops.ChainLauncher(y, t_buf, ft, d, True, write_values=True)
+        t_buf = torch.empty((B, P) if S is None else (S, B, P), dtype=torch.float32, device=dev)
+        plain = ops.ChainLauncher(y, t_buf, ft, d, True, write_values=True, draws=S)
+
+        def gemm():
+            if S is None:
+                torch.addmm(bd, h, Wd, out=t_buf)
+            else:
+                torch.baddbmm(bd[:, None, :], h, Wd, out=t_buf)
+
         for _ in range(3):
-            torch.addmm(bd, h, Wd, out=t_buf)
+            gemm()
             plain.launch(sh)
         pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
         for e0, e1 in pairs:
             e0.record(stream)
-            torch.addmm(bd, h, Wd, out=t_buf)
+            gemm()
             plain.launch(sh)
             e1.record(stream)
         torch.cuda.synchronize()
@@ -366,7 +380,8 @@ def main():
         if grad_mode:
             bytes_launch = algorithmic_bytes_grad(d, P, B)
         elif dense_mode:
-            bytes_launch = float(B) * (4 * args.hidden + 4 * d + 4) + 4.0 * args.hidden * P + 4.0 * P
+            nd = 1 if S is None else S
+            bytes_launch = float(B) * (4 * args.hidden * nd + 4 * d + 4) + nd * (4.0 * args.hidden * P + 4.0 * P)
         else:
             bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
@@ -385,11 +400,15 @@ def main():
             "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
         }[args.config]
         if grad_mode:
-            kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group_kernel"
+            kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group1_kernel"
             metric = f"log_prob backward evals/sec (whole node), {args.config}"
         elif dense_mode:
-            kernel_name = "chain_dense_kernel"
-            metric = f"Dense(H={args.hidden})->log_prob evals/sec (whole node), {args.config}"
+            if S is None:
+                kernel_name = "chain_dense1_kernel" if d == 1 else "chain_dense_kernel"
+                metric = f"Dense(H={args.hidden})->log_prob evals/sec (whole node), {args.config}"
+            else:
+                kernel_name = "posterior_dense1_kernel" if d == 1 else "posterior_dense_kernel"
+                metric = f"DenseVariational(H={args.hidden})->posterior (draw, sample) evals/sec (whole node), {args.config}"
         else:
             kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel",
                            "C5": "chain_persistent_kernel + posterior_merge_kernel"}[args.config]

@@ -373,6 +373,38 @@ class DenseLauncher:
         return self.sum
 
 
+class PosteriorDenseLauncher(DenseLauncher):
+    """Pre-bound fused DenseVariational->posterior launch (``nfn_posterior_lse_dense_f32``):
+    ``h`` (S, B, H), ``W`` (S, H, P), ``b`` (S, P) or None."""
+
+    def __init__(self, y: torch.Tensor, h: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor],
+                 flow_types: Sequence[str], n_dims: int, trainable_base: bool, write_values: bool = True):
+        self.lib = _lib.load()
+        dev = y.device
+        self.n_dims = int(n_dims)
+        self.P = total_param_size(flow_types, n_dims, trainable_base)
+        self.S, self.B, self.H = (int(v) for v in h.shape)
+        assert dense_fusable(self.H, self.P, self.n_dims) and h.is_contiguous()
+        assert tuple(W.shape) == (self.S, self.H, self.P) and (b is None or tuple(b.shape) == (self.S, self.P))
+        self.y, self.h, self.W = y, h, W.contiguous()
+        self.b = None if b is None else b.contiguous()
+        self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
+        self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
+        self.partials = torch.empty((max(1, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
+                                    dtype=torch.float64, device=dev)
+        self._ids, self._k = flow_ids(flow_types)
+        self._args = (
+            _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), int(h.stride(1)), self.H, _ptr(self.W),
+            self.H * self.P, _ptr(self.b), self.P, self.S, self.B, self.n_dims, ctypes.cast(self._ids, ctypes.c_void_p),
+            self._k, int(bool(trainable_base)), None, None, _ptr(self.out), None, _ptr(self.partials),
+        )
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self.lib.nfn_posterior_lse_dense_f32(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_posterior_lse_dense_f32")
+
+
 def chain_sample(eps, t, flow_types: Sequence[str], n_dims: int, trainable_base: bool, y_mean=None, y_std=None,
                  want_log_prob: bool = True):
     """Draw ``y ~ p(y | t)`` through the inverted flows for given standard-normal ``eps``

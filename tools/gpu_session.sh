@@ -89,6 +89,15 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --config C5 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_c5" -o w -- \
         python3 "$ROOT/bench.py" --config C5 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    dense_c5) run bench_dense_c5 300 python bench.py --mode dense --config C5 --steps 50 --warmup 10 --cpu-seconds 8 ;;
+    prof_dense_c5)
+      { cd /tmp; run rocprof_dense_c5 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_dense_c5" -o densec5 -- \
+        python3 "$ROOT/bench.py" --mode dense --config C5 --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_grad_c3)
+      { cd /tmp; run pmc_fetch_grad_c3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_grad_c3" -o f -- \
+        python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write_grad_c3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_grad_c3" -o w -- \
+        python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
