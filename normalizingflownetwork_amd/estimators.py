@@ -290,7 +290,8 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
     (``BayesianNNEstimator.py:92-107``); each posterior draw re-samples the MLP
     weights and yields a ``t`` draw.  ``score`` stacks the S draws as
     ``t (S, B, P)`` and evaluates ``logsumexp_s(log_pdf) - log S`` per sample in
-    ONE fused kernel (``nfn_posterior_lse_f32``) instead of S model re-runs."""
+    ONE fused kernel (``nfn_posterior_lse_f32``, or ``nfn_posterior_lse_dense_f32`` with the
+    output layer fused) instead of S model re-runs."""
 
     def __init__(self, n_dims, kl_weight_scale=1.0, n_flows=2, trainable_base_dist=True, flow_types=None,
                  hidden_sizes=(10,), activation="tanh", noise_reg=("fixed_rate", 0.0), learning_rate=2e-2,
@@ -307,8 +308,10 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
                          random_seed=random_seed, noise_reg=noise_reg)
         self._draw_gen = None
 
-    def params_draws(self, x, n_draws: int) -> torch.Tensor:
-        """``t`` for ``n_draws`` posterior weight samples: (S, B, P)."""
+    def _last_layer_draws(self, x, n_draws: int):
+        """Per posterior draw: the last hidden activations and the sampled output layer,
+        ``h (S, B, H)``, ``W (S, H, P)``, ``b (S, P)`` (every layer re-sampled per draw,
+        ``BayesianNNEstimator.py:122-145``)."""
         x = ops.as_device_f32(x)
         if x.dim() == 1:
             x = x.unsqueeze(-1)
@@ -322,7 +325,7 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
         xs = torch.as_tensor(self.x_std, dtype=torch.float32, device=dev)
         xn = (x - xm) / (xs + 1e-8)
         act = _ACTIVATIONS[self.activation]
-        draws = []
+        hs, ws, bs = [], [], []
         for _ in range(n_draws):
             h = xn
             n = len(self._mlp.weights)
@@ -332,17 +335,26 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
                                                                dtype=torch.float32)
                     b = b + self.posterior_scale * torch.randn(b.shape, generator=self._draw_gen, device=dev,
                                                                dtype=torch.float32)
-                h = h @ w + b
                 if i < n - 1:
-                    h = act(h)
-            draws.append(h)
-        return torch.stack(draws).contiguous()
+                    h = act(h @ w + b)
+                else:
+                    hs.append(h)
+                    ws.append(w)
+                    bs.append(b)
+        return torch.stack(hs).contiguous(), torch.stack(ws).contiguous(), torch.stack(bs).contiguous()
+
+    def params_draws(self, x, n_draws: int) -> torch.Tensor:
+        """``t`` for ``n_draws`` posterior weight samples: (S, B, P)."""
+        h, W, b = self._last_layer_draws(x, n_draws)
+        return torch.matmul(h, W) + b[:, None, :]
 
     def score(self, x_data, y_data, n_draws: Optional[int] = None) -> float:
-        """``BayesianNNEstimator.py:65-76``: 50 draws (1 in map mode)."""
+        """``BayesianNNEstimator.py:65-76``: 50 draws (1 in map mode).  The output layer is
+        fused into the posterior kernel (``nfn_posterior_lse_dense_f32``: t_s = h_s W_s + b_s
+        never written to memory) when its width allows, else t is formed by the library GEMM."""
         S = n_draws if n_draws is not None else (1 if self.map_mode else 50)
-        t = self.params_draws(np.asarray(x_data, np.float32), S)
-        _, s = ops.posterior_lse(np.asarray(y_data, np.float32), t, self.dist_layer.flow_types, self.n_dims,
-                                 self.dist_layer.trainable_base_dist, self.y_mean, self.y_std,
-                                 want_values=False, want_sum=True)
+        h, W, b = self._last_layer_draws(np.asarray(x_data, np.float32), S)
+        _, s = ops.posterior_lse_dense(np.asarray(y_data, np.float32), h, W, b, self.dist_layer.flow_types,
+                                       self.n_dims, self.dist_layer.trainable_base_dist, self.y_mean, self.y_std,
+                                       want_values=False, want_sum=True)
         return float(s.item()) / int(np.shape(y_data)[0])

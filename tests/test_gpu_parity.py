@@ -220,6 +220,17 @@ def test_estimators_end_to_end(gpu):
     bnn.set_data_normalization(x, y)
     bs = bnn.score(x[:512], y[:512], n_draws=4)
     assert np.isfinite(bs)
+    # H = 16: the score runs the fused DenseVariational posterior kernel; the same
+    # posterior draws (re-seeded) through the oracle on t = h W + b
+    bnn16 = BayesNormalizingFlowNetwork(n_dims=1, n_flows=2, hidden_sizes=(16,))
+    bnn16.set_data_normalization(x, y)
+    bnn16._draw_gen = None
+    s16 = bnn16.score(x[:512], y[:512], n_draws=4)
+    bnn16._draw_gen = None
+    td = bnn16.params_draws(x[:512], 4).cpu().numpy()
+    r64 = O.posterior_lse(y[:512], td, ("radial", "radial"), 1, True, bnn16.y_mean, bnn16.y_std)
+    r32 = O.posterior_lse(y[:512], td, ("radial", "radial"), 1, True, bnn16.y_mean, bnn16.y_std, np.float32)
+    assert abs(s16 - r64.mean()) <= O.tolerance_bound(r64, r32).mean() + 1e-6
 
 
 # ---------------------------------------------------------------------------
