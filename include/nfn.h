@@ -226,6 +226,26 @@ int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t,
                               double* workspace, void* stream);
 
 /*
+ * Backward of nfn_chain_logprob_dense_f32 (the training step through the output Dense
+ * layer and the flow chain, MaximumLikelihoodNNEstimator.py:37-44 + BaseEstimator.py:19-31),
+ * for L = sum_b g_out[b] * logp_b (g_out NULL = ones), t = h W + b never written:
+ *   grad_h : (B, H) at grad_h_rowstride, dL/dh = dt W^T      (nullable)
+ *   grad_W : (H, P) = sum_b h_b^T dt_b;  grad_b : (P,) = sum_b dt_b   (nullable; overwritten,
+ *            fixed-order reduction: bitwise deterministic)
+ *   grad_y : (B, d) contiguous (nullable);  out_logp : (B,) (nullable)
+ *   workspace : device float[nfn_dense_grad_workspace_floats(B, H, P)] (needed with grad_W / grad_b)
+ * Shapes as nfn_chain_logprob_dense_f32 (H in {4..64}, P <= 64, d <= 8), and the tile's
+ * flow inputs must fit LDS; other shapes return NFN_E_SHAPE.
+ */
+int64_t nfn_dense_grad_workspace_floats(int64_t B, int32_t H, int32_t P);
+int32_t nfn_chain_logprob_dense_grad_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride,
+                                         int32_t H, const float* W, const float* bias, int64_t B, int32_t d,
+                                         const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                                         const float* y_mean, const float* y_std, const float* g_out,
+                                         float* out_logp, float* grad_h, int64_t grad_h_rowstride, float* grad_W,
+                                         float* grad_b, float* grad_y, float* workspace, void* stream);
+
+/*
  * Bayesian posterior score with the output DenseVariational layer fused
  * (BayesianNNEstimator.py:65-76 score, :136-145 the variational output layer):
  *   out_lse[b] = logsumexp_s( logp(y_b | t_sb = h_sb W_s + bias_s) [- sum log y_std] ) - log(S)

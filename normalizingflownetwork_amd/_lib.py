@@ -53,6 +53,12 @@ SIGNATURES = {
         [_vp, _c_int64, _vp, _c_int64, _c_int32, _vp, _vp, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp,
          _vp, _vp, _vp, _vp],
     ),
+    "nfn_dense_grad_workspace_floats": (_c_int64, [_c_int64, _c_int32, _c_int32]),
+    "nfn_chain_logprob_dense_grad_f32": (
+        _c_int32,
+        [_vp, _c_int64, _vp, _c_int64, _c_int32, _vp, _vp, _c_int64, _c_int32, _vp, _c_int32, _c_int32, _vp, _vp,
+         _vp, _vp, _vp, _c_int64, _vp, _vp, _vp, _vp, _vp],
+    ),
     "nfn_posterior_lse_dense_f32": (
         _c_int32,
         [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _c_int64, _vp, _c_int64, _c_int32, _c_int64,

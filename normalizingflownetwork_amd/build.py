@@ -35,6 +35,7 @@ UNITS = [
     ("grad_group_precise", "nfn_grad_group.hip", ["-DNFN_FAST=0"]),
     ("grid", "nfn_grid.hip", []),
     ("dense", "nfn_dense.hip", []),
+    ("dense_grad", "nfn_dense_grad.hip", []),
     ("sample", "nfn_sample.hip", []),
     ("comm", "nfn_comm.hip", []),
 ]

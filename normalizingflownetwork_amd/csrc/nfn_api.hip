@@ -508,6 +508,77 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   return rc;
 }
 
+constexpr int64_t kDenseGradMaxParts = 2048;  // per-workgroup partials (>= CUs x resident workgroups)
+
+int64_t dense_grad_parts(int64_t B) { return std::max<int64_t>(1, std::min<int64_t>(kDenseGradMaxParts, ((B + 63) / 64 + 3) / 4)); }
+
+int32_t run_dense_grad(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride, int32_t H,
+                       const float* W, const float* bias, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
+                       int32_t trainable_base, const float* y_mean, const float* y_std, const float* g_out,
+                       float* out_logp, float* grad_h, int64_t grad_h_rowstride, float* grad_W, float* grad_b,
+                       float* grad_y, float* workspace, void* stream) {
+  g_last_error.clear();
+  DenseGradArgs g;
+  memset(&g, 0, sizeof(g));
+  DenseArgs& da = g.da;
+  ChainArgs& a = da.c;
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (P < 0) return P;
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");
+  if (H < 4 || H > 64 || (H & (H - 1)) != 0) return fail(NFN_E_SHAPE, "hidden width H must be 4, 8, 16, 32 or 64");
+  if (P < 1 || P > 64) return fail(NFN_E_SHAPE, "fused dense path needs 1 <= P <= 64");
+  if (d > 8) return fail(NFN_E_SHAPE, "fused dense path needs n_dims <= 8");
+  if (h_rowstride < H || (h_rowstride & 3) != 0) return fail(NFN_E_SHAPE, "h row stride must be >= H and a multiple of 4");
+  if (grad_h && grad_h_rowstride < H) return fail(NFN_E_SHAPE, "grad_h row stride < H");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nWb = H * P + P;
+  if (B == 0) {
+    if (grad_W && hipMemsetAsync(grad_W, 0, sizeof(float) * H * P, s) != hipSuccess) return check_hip("hipMemsetAsync");
+    if (grad_b && hipMemsetAsync(grad_b, 0, sizeof(float) * P, s) != hipSuccess) return check_hip("hipMemsetAsync");
+    return NFN_OK;
+  }
+  if (!y || !h || !W) return fail(NFN_E_NULLPTR, "y, h or W is NULL");
+  if ((reinterpret_cast<uintptr_t>(h) & 15) != 0) return fail(NFN_E_SHAPE, "h must be 16-byte aligned");
+  if ((grad_W || grad_b) && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but grad_W / grad_b requested");
+  const int S = P | 1;
+  const int NP = ((P + 15) / 16) * 16;
+  const size_t lds = (size_t)(H * NP + 4 * (64 * (H | 1) + 64 * S + K * d * 64) + nWb) * sizeof(float);
+  if (lds > (size_t)160 * 1024) return fail(NFN_E_SHAPE, "fused dense backward: tile + flow inputs exceed LDS");
+  a.y = y;
+  a.y_mean = y_mean;
+  a.y_std = y_std;
+  a.out = out_logp;
+  a.y_bstride = y_bstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = S;
+  a.trainable = trainable_base ? 1 : 0;
+  a.S = 1;
+  a.ntiles = (B + 63) / 64;
+  da.h = h;
+  da.h_rowstride = h_rowstride;
+  da.W = W;
+  da.bias = bias;
+  da.H = H;
+  da.h_lds_stride = H | 1;
+  g.g_out = g_out;
+  g.grad_h = grad_h;
+  g.gh_rowstride = grad_h ? grad_h_rowstride : 0;
+  g.grad_y = grad_y;
+  g.part = (grad_W || grad_b) ? workspace : nullptr;  // no partials without grad_W / grad_b
+  const int64_t nparts = launch_dense_grad(use_fast_math(), dm_for(d), g, lds, dense_grad_parts(B), s);
+  if (nparts == 0) return fail(NFN_E_SHAPE, "no fused dense backward instance for this shape");
+  int32_t rc = check_hip("chain_dense_grad_kernel launch");
+  if (rc == NFN_OK && (grad_W || grad_b)) {
+    launch_sum_partials(g.part, nparts, nWb, grad_W, grad_b, H * P, s);
+    rc = check_hip("sum_partials_kernel launch");
+  }
+  return rc;
+}
+
 int32_t run_sample(const float* eps, int64_t eps_bstride, const float* t, int64_t t_rowstride, int64_t B, int32_t d,
                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                    const float* y_std, float* y_out, float* logp_out, void* stream) {
@@ -687,6 +758,20 @@ int32_t nfn_chain_logprob_dense_f32(const float* y, int64_t y_bstride, const flo
                                     void* stream) {
   return run_dense(y, y_bstride, h, h_rowstride, H, W, bias, B, d, flow_ids, K, trainable_base, y_mean, y_std,
                    out_logp, out_sum, workspace, stream);
+}
+
+int64_t nfn_dense_grad_workspace_floats(int64_t B, int32_t H, int32_t P) {
+  return (int64_t)(H * P + P) * dense_grad_parts(B < 0 ? 0 : B);
+}
+
+int32_t nfn_chain_logprob_dense_grad_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride,
+                                         int32_t H, const float* W, const float* bias, int64_t B, int32_t d,
+                                         const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                                         const float* y_mean, const float* y_std, const float* g_out,
+                                         float* out_logp, float* grad_h, int64_t grad_h_rowstride, float* grad_W,
+                                         float* grad_b, float* grad_y, float* workspace, void* stream) {
+  return run_dense_grad(y, y_bstride, h, h_rowstride, H, W, bias, B, d, flow_ids, K, trainable_base, y_mean, y_std,
+                        g_out, out_logp, grad_h, grad_h_rowstride, grad_W, grad_b, grad_y, workspace, stream);
 }
 
 int32_t nfn_posterior_lse_dense_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_drawstride,

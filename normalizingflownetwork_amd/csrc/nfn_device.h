@@ -115,6 +115,16 @@ struct DenseArgs {
   int64_t b_drawstride;
 };
 
+// Fused output Dense layer, backward (nfn_dense_grad.hip).
+struct DenseGradArgs {
+  DenseArgs da;
+  const float* g_out;    // upstream gradient (B,) or NULL = ones
+  float* grad_h;         // (B, H) at gh_rowstride, or NULL
+  int64_t gh_rowstride;
+  float* grad_y;         // (B, d) contiguous, or NULL
+  float* part;           // per-workgroup partial [grad_W (H x P) | grad_b (P)]
+};
+
 // Sampling through the inverted flows (nfn_sample.hip).
 struct SampleArgs {
   ChainArgs c;

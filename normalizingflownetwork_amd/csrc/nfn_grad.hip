@@ -41,54 +41,6 @@ __device__ __forceinline__ void store_rows(const float* lds, float* __restrict__
   }
 }
 
-// One sample: forward from z (already normalised), keeping each flow's input in
-// zh[(k * d + j) * zs] (LDS), then the reverse pass; the parameter row `row` (LDS)
-// is overwritten in place with d logp / d t.  Returns log_prob (without the
-// -sum(log y_std) correction); `adj` receives d logp / d z_0.
-template <int DM, bool FAST>
-__device__ __forceinline__ float grad_sample(float (&z)[DM], float* row, float* zh, int zs, const ChainArgs& a,
-                                             float gl, float (&adj)[DM]) {
-  const int d = a.d;
-  const int K = a.prog.K;
-  float lp;
-  if constexpr (DM == 1 && FAST) {
-    if (K <= 16) {
-      float a1;
-      const float lp1 = grad1_packed(z[0], row, zh, zs, a.prog.types[0], K, a.P, a.trainable != 0, gl,
-                                     a.out != nullptr, a1);
-      adj[0] = a1;
-      return lp1;
-    }
-  }
-  {
-    float ildj = 0.0f;
-    for (int k = 0; k < K; ++k) {
-      const int st = a.prog.step[k];
-#pragma unroll
-      for (int j = 0; j < DM; ++j)
-        if (j < d) zh[(k * d + j) * zs] = z[j];
-      ildj = ildj + flow_step<DM, FAST>(st & 3, z, row + (st >> 2), d);
-    }
-    lp = base_log_prob<DM, FAST>(z, row, d, a.trainable != 0) + ildj;
-  }
-  base_bwd<DM, FAST>(z, adj, row, d, a.trainable != 0, gl);
-  for (int k = K - 1; k >= 0; --k) {
-    const int st = a.prog.step[k];
-    float zk[DM];
-#pragma unroll
-    for (int j = 0; j < DM; ++j) zk[j] = j < d ? zh[(k * d + j) * zs] : 0.0f;
-    float* p = row + (st >> 2);
-    const int id = st & 3;
-    if (id == NFN_FLOW_PLANAR)
-      planar_bwd<DM, FAST>(zk, adj, p, d, gl);
-    else if (id == NFN_FLOW_RADIAL)
-      radial_bwd<DM, FAST>(zk, adj, p, d, gl);
-    else
-      affine_bwd<DM, FAST>(zk, adj, p, d, gl);
-  }
-  return lp;
-}
-
 template <int DM, bool FAST>
 __device__ __forceinline__ void store_grad_y(const GradArgs& ga, int64_t b, const float (&adj)[DM]) {
   const ChainArgs& a = ga.c;

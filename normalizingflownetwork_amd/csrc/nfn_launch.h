@@ -70,6 +70,9 @@ __host__ __device__ inline int dense1_wave_floats(int P, int SH) { return std::m
 // nfn_dense.hip; false if (dm, H) has no instance
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_posterior_dense(bool fast, int dm, const DenseArgs& da, hipStream_t s, int64_t* grid);
+// nfn_dense_grad.hip: returns the number of per-workgroup partials written (0 = no instance)
+int64_t launch_dense_grad(bool fast, int dm, const DenseGradArgs& g, size_t lds, int64_t max_parts, hipStream_t s);
+void launch_sum_partials(const float* part, int64_t nparts, int n, float* gW, float* gb, int nW, hipStream_t s);
 // nfn_sample.hip
 void launch_sample(bool fast, int dm, const SampleArgs& sa, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_grid.hip

@@ -276,6 +276,70 @@ def chain_log_prob_dense(
     return out, osum
 
 
+def chain_log_prob_dense_grad(
+    y,
+    h,
+    W,
+    b,
+    flow_types: Sequence[str],
+    n_dims: int,
+    trainable_base: bool,
+    y_mean=None,
+    y_std=None,
+    g_out=None,
+    want_logp: bool = False,
+):
+    """Backward of :func:`chain_log_prob_dense` (one fused kernel + a fixed-order reduction):
+    for ``L = sum_b g_out[b] * log_prob_b`` returns ``(log_prob | None, dL/dh (B, H),
+    dL/dW (H, P), dL/db (P,), dL/dy (B, d))`` — what Keras autodiff takes through the output
+    ``Dense(P)`` and the layer's ``log_prob`` when the reference trains
+    (``MaximumLikelihoodNNEstimator.py:37-44``, ``BaseEstimator.py:19-31``), with ``t`` never
+    materialised.  Shapes the fused kernel does not take run as library GEMMs around
+    :func:`chain_log_prob_grad`."""
+    dev = _device()
+    P = total_param_size(flow_types, n_dims, trainable_base)
+    h = as_device_f32(h, dev)
+    assert h.dim() == 2, "h must be (B, H)"
+    B, H = int(h.shape[0]), int(h.shape[1])
+    W = as_device_f32(W, dev).contiguous()
+    assert tuple(W.shape) == (H, P), f"W must be ({H}, {P})"
+    bb = None if b is None else as_device_f32(b, dev).reshape(-1).contiguous()
+    y = _prep_2d(y, n_dims, "y", dev)
+    assert y.shape[0] in (1, B), "incompatible batch sizes"
+    g = None
+    if g_out is not None:
+        g = as_device_f32(g_out, dev).reshape(-1).contiguous()
+        assert g.numel() == B, f"g_out must have {B} elements"
+    lib = _lib.load()
+    rc = _lib.NFN_E_SHAPE
+    if dense_fusable(H, P, n_dims) and h.stride(0) % 4 == 0 and h.data_ptr() % 16 == 0:
+        ym = ys = None
+        if y_mean is not None:
+            ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
+            ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+        lp = torch.empty((B,), dtype=torch.float32, device=dev) if want_logp else None
+        gh = torch.empty((B, H), dtype=torch.float32, device=dev)
+        gW = torch.empty((H, P), dtype=torch.float32, device=dev)
+        gb = torch.empty((P,), dtype=torch.float32, device=dev)
+        gy = torch.empty((B, n_dims), dtype=torch.float32, device=dev)
+        ws = torch.empty((max(1, int(lib.nfn_dense_grad_workspace_floats(B, H, P))),), dtype=torch.float32,
+                         device=dev)
+        ids, k = flow_ids(flow_types)
+        rc = lib.nfn_chain_logprob_dense_grad_f32(
+            _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), H, _ptr(W), _ptr(bb), B, int(n_dims),
+            ctypes.cast(ids, ctypes.c_void_p), k, int(bool(trainable_base)), _ptr(ym), _ptr(ys), _ptr(g), _ptr(lp),
+            _ptr(gh), H, _ptr(gW), _ptr(gb), _ptr(gy), _ptr(ws), _stream(),
+        )
+        if rc == 0:
+            return lp, gh, gW, gb, gy
+        if rc != _lib.NFN_E_SHAPE:
+            _lib.check(rc, "nfn_chain_logprob_dense_grad_f32")
+    # unfused: t by the library GEMM, the chain backward kernel, library GEMMs for dh / dW / db
+    t = h @ W + (bb if bb is not None else 0.0)
+    lp, gt, gy = chain_log_prob_grad(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, g, want_logp)
+    return lp, gt @ W.t(), h.t() @ gt, gt.sum(0), gy
+
+
 def posterior_lse_dense(
     y,
     h,

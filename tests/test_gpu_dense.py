@@ -153,3 +153,79 @@ def test_posterior_dense_full_size_c5_sampled(gpu):
     got = out[idx.cuda()].cpu().numpy()
     assert np.all(np.abs(got - ref64) <= O.tolerance_bound(ref64, ref32))
     assert abs(s.item() - out.double().sum().item()) <= 1e-9 * abs(s.item()) + 1e-6
+
+
+@pytest.mark.parametrize("ft,d,H,B", [(("planar", "radial") * 5, 1, 16, 1000), (("radial", "radial"), 1, 4, 333),
+                                      (("affine", "planar", "radial"), 3, 8, 300), (("planar", "affine"), 8, 16, 129),
+                                      (("radial",) * 14, 1, 32, 201)])
+def test_dense_grad_matches_oracle(math_mode, ft, d, H, B):
+    """Backward through the fused output Dense layer + chain (nfn_chain_logprob_dense_grad_f32):
+    dL/dh = dt W^T, dL/dW = h^T dt, dL/db = sum dt, dL/dy — against the autodiff oracle's dt
+    (fp64, at the fp32 t) pushed through the same products in fp64.  Bounds: the oracle's
+    per-element dt tolerance carried through |W| / |h|, plus 1e-5 of the products' magnitudes
+    (fp32 MFMA accumulation)."""
+    from oracle import nfn_grad_oracle as G
+    from normalizingflownetwork_amd import ops
+
+    h, W, b, y, t64, t32 = _case(ft, d, H, B, seed=3 * H + B)
+    rng = np.random.default_rng(B)
+    g = rng.standard_normal(B).astype(np.float32)
+    lp, gh, gW, gb, gy = ops.chain_log_prob_dense_grad(torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(),
+                                                       torch.from_numpy(W).cuda(), torch.from_numpy(b).cuda(), ft, d,
+                                                       True, g_out=torch.from_numpy(g).cuda(), want_logp=True)
+    gt64, gy64, dev_t, dev_y = G.fp32_spread(y, t32, ft, d, True, g_out=g)
+    bt = G.grad_tolerance(gt64, dev_t)
+    fin = np.isfinite(gt64).all(1)
+    assert fin.all(), "oracle non-finite on this case"
+    W64, h64 = W.astype(np.float64), h.astype(np.float64)
+    gh_ref, gW_ref, gb_ref = gt64 @ W64.T, h64.T @ gt64, gt64.sum(0)
+    bh = bt @ np.abs(W64).T + 1e-5 * (np.abs(gt64) @ np.abs(W64).T) + 1e-7
+    bW = np.abs(h64).T @ bt + 1e-5 * (np.abs(h64).T @ np.abs(gt64)) + 1e-6
+    bb = bt.sum(0) + 1e-5 * np.abs(gt64).sum(0) + 1e-6
+    for got, ref, bound, what in ((gh, gh_ref, bh, "dh"), (gW, gW_ref, bW, "dW"), (gb, gb_ref, bb, "db")):
+        err = np.abs(got.cpu().numpy().astype(np.float64) - ref)
+        assert (err <= bound).all(), f"{what}: max err/bound {np.max(err / bound):.3g}"
+    ey = np.abs(gy.cpu().numpy() - gy64)
+    assert (ey <= G.grad_tolerance(gy64, dev_y)).all(), "dy"
+    ref64 = O.chain_log_prob(y, t64, ft, d, True, np.float64)
+    ref32 = O.chain_log_prob(y, t32, ft, d, True, np.float32)
+    assert np.all(np.abs(lp.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32))
+    # deterministic: a second run is bitwise identical
+    _, gh2, gW2, gb2, _ = ops.chain_log_prob_dense_grad(torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(),
+                                                         torch.from_numpy(W).cuda(), torch.from_numpy(b).cuda(), ft,
+                                                         d, True, g_out=torch.from_numpy(g).cuda())
+    assert torch.equal(gh, gh2) and torch.equal(gW, gW2) and torch.equal(gb, gb2)
+
+
+def test_dense_grad_fallback_and_full_size(gpu):
+    """The unfused fallback (H = 12) agrees with the fused kernel's formulas, and at the C2
+    batch (2^24, H = 16) the fused backward is finite and matches the unfused path
+    (library GEMM t + chain backward kernel + library GEMMs) within fp32 rounding."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d = ("planar", "radial") * 5, 1
+    P = O.total_param_size(ft, d, True)
+    B, H = 1 << 24, 16
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    h = torch.randn((B, H), generator=gen, device="cuda")
+    W = torch.randn((H, P), generator=gen, device="cuda") / 4.0
+    b = 0.1 * torch.randn((P,), generator=gen, device="cuda")
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    g = torch.full((B,), 1.0 / B, device="cuda")
+    _, gh, gW, gb, gy = ops.chain_log_prob_dense_grad(y, h, W, b, ft, d, True, g_out=g)
+    assert torch.isfinite(gh).all() and torch.isfinite(gW).all() and torch.isfinite(gb).all()
+    _, gt, gyr = ops.chain_log_prob_grad(y, torch.addmm(b, h, W), ft, d, True, g_out=g)
+    # t differs by fp32 rounding between the two paths (MFMA vs library GEMM): per-row
+    # gradients agree except on the rare ill-conditioned rows; the batch sums agree to
+    # a small fraction of their magnitude sums (a layout error would be O(1))
+    for got, ref in ((gh, gt @ W.t()), (gy, gyr)):
+        rel = (got - ref).abs() / (ref.abs() + 1e-6 * ref.abs().max())
+        assert (rel > 1e-3).double().mean().item() < 1e-4
+    gt64 = gt.double()
+    assert ((gW.double() - h.double().t() @ gt64).abs() <= 1e-3 * (h.double().abs().t() @ gt64.abs())).all()
+    assert ((gb.double() - gt64.sum(0)).abs() <= 1e-3 * gt64.abs().sum(0)).all()
+    h12 = torch.randn((300, 12), generator=gen, device="cuda")
+    W12 = torch.randn((12, P), generator=gen, device="cuda") / 4.0
+    _, gh12, gW12, gb12, _ = ops.chain_log_prob_dense_grad(y[:300], h12, W12, b, ft, d, True)
+    _, gt12, _ = ops.chain_log_prob_grad(y[:300], h12 @ W12 + b, ft, d, True)
+    torch.testing.assert_close(gW12, h12.t() @ gt12)

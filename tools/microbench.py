@@ -212,8 +212,55 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
                           "rounds_ms": times[k]}), flush=True)
 
 
+def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
+    """C2 training step through the output Dense layer: the fused backward (t never
+    written) vs the unfused path (library GEMM t, chain backward kernel, GEMMs for
+    dh / dW and the db sum) vs the chain backward alone on a resident t."""
+    ft, d = ("planar", "radial") * 5, 1
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    h = torch.randn((B, H), generator=gen, device="cuda")
+    W = torch.randn((H, P), generator=gen, device="cuda") / float(np.sqrt(H))
+    b = 0.1 * torch.randn((P,), generator=gen, device="cuda")
+    g = torch.full((B,), -1.0 / B, device="cuda")
+    t = torch.addmm(b, h, W)
+
+    def unfused():
+        tt = torch.addmm(b, h, W)
+        _, gt, gy = ops.chain_log_prob_grad(y, tt, ft, d, True, g_out=g)
+        return gt @ W.t(), h.t() @ gt, gt.sum(0), gy
+
+    fns = {
+        "fused": lambda: ops.chain_log_prob_dense_grad(y, h, W, b, ft, d, True, g_out=g),
+        "unfused": unfused,
+        "chain_backward_on_resident_t": lambda: ops.chain_log_prob_grad(y, t, ft, d, True, g_out=g),
+    }
+    stream = torch.cuda.current_stream()
+    prewarm(fns["fused"])
+    times = {k: [] for k in fns}
+    for r in range(rounds):
+        for k, fn in fns.items():
+            for _ in range(3):
+                fn()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in evs:
+                e0.record(stream)
+                fn()
+                e1.record(stream)
+            torch.cuda.synchronize()
+            times[k].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+    for k in fns:
+        ms = float(np.median(times[k]))
+        print(json.dumps({"cfg": "C2", "mode": "dense_grad", "H": H, "B": B, "variant": k, "ms": ms,
+                          "evals_per_s": B / ms * 1e3, "rounds_ms": times[k]}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "dgrad":
+        run_dense_grad()
+        return
     if which[0] == "pdense":
         run_posterior_dense()
         return
