@@ -93,6 +93,9 @@ class BaseEstimator:
         self.y_mean = np.zeros((self.n_dims,), np.float32)
         self.y_std = np.ones((self.n_dims,), np.float32)
         self._mlp = None
+        # fit: the output Dense layer fused into the chain kernels (forward + backward)
+        # when its shapes allow; False trains through the materialised t instead
+        self.fused_dense = True
         if n_dims_x is not None:
             self._build(n_dims_x)
 
@@ -219,6 +222,10 @@ class BaseEstimator:
         self._mlp.weights, self._mlp.biases = params[:nw], params[nw:]
         lr = getattr(self, "learning_rate", 3e-3)
         opt = torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-7)  # Keras Adam defaults
+        dl = self.dist_layer
+        P = ops.total_param_size(dl.flow_types, self.n_dims, dl.trainable_base_dist)
+        fused_dense = (len(self._mlp.weights) > 1 and self.fused_dense
+                       and ops.dense_fusable(int(self._mlp.weights[-1].shape[0]), P, self.n_dims))
         batch_size = 32 if batch_size is None else int(batch_size)
         epochs = 1 if epochs is None else int(epochs)
         X = torch.from_numpy(x).to(dev)
@@ -242,8 +249,13 @@ class BaseEstimator:
                     yc = (Y[idx] - ym) / ys
                     if self.y_noise_std > 0:
                         yc = yc + self.y_noise_std * torch.randn(yc.shape, generator=gen, device=dev)
-                    t = self._mlp(xn)
-                    lp = ops.log_prob(yc, t, dl.flow_types, self.n_dims, dl.trainable_base_dist)
+                    if fused_dense:  # output layer fused into the chain, forward and backward
+                        lp = ops.log_prob_dense(yc, self._mlp.hidden(xn), self._mlp.weights[-1],
+                                                self._mlp.biases[-1], dl.flow_types, self.n_dims,
+                                                dl.trainable_base_dist)
+                    else:
+                        t = self._mlp(xn)
+                        lp = ops.log_prob(yc, t, dl.flow_types, self.n_dims, dl.trainable_base_dist)
                     loss = -lp.mean() + sum_log_ys
                     opt.zero_grad(set_to_none=True)
                     loss.backward()

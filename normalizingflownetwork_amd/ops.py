@@ -219,6 +219,39 @@ def log_prob(y, t, flow_types: Sequence[str], n_dims: int, trainable_base: bool,
     return _ChainLogProb.apply(y, t, tuple(flow_types), int(n_dims), bool(trainable_base), y_mean, y_std)
 
 
+class _DenseLogProb(torch.autograd.Function):
+    """``log_prob(y | t = h W + b)`` as a differentiable op with the output Dense layer
+    fused both ways: forward = ``nfn_chain_logprob_dense_f32``, backward =
+    ``nfn_chain_logprob_dense_grad_f32`` (t is never materialised)."""
+
+    @staticmethod
+    def forward(ctx, y, h, W, b, flow_types, n_dims, trainable_base):
+        out, _ = chain_log_prob_dense(y, h, W, b, flow_types, n_dims, trainable_base)
+        ctx.save_for_backward(y, h, W, b)
+        ctx.meta = (tuple(flow_types), int(n_dims), bool(trainable_base))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, h, W, b = ctx.saved_tensors
+        flow_types, n_dims, trainable_base = ctx.meta
+        _, gh, gW, gb, gy = chain_log_prob_dense_grad(y, h, W, b, flow_types, n_dims, trainable_base,
+                                                      g_out=g.contiguous())
+        if y.shape[0] == 1 and gh.shape[0] > 1:
+            gy = gy.sum(0, keepdim=True)
+        return gy, gh, gW, gb, None, None, None
+
+
+def log_prob_dense(y, h, W, b, flow_types: Sequence[str], n_dims: int, trainable_base: bool):
+    """Differentiable ``log_prob(y | h W + b)`` (B,) through the fused Dense layer: the
+    gradients w.r.t. ``h``, ``W``, ``b`` (and ``y``) come from the fused backward kernel."""
+    dev = _device()
+    y = _prep_2d(y, n_dims, "y", dev)
+    h = as_device_f32(h, dev).contiguous()
+    return _DenseLogProb.apply(y, h, as_device_f32(W, dev), as_device_f32(b, dev), tuple(flow_types), int(n_dims),
+                               bool(trainable_base))
+
+
 DENSE_HIDDEN_WIDTHS = (4, 8, 16, 32, 64)
 
 

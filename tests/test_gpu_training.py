@@ -137,3 +137,51 @@ def test_noise_off_at_evaluation(gpu):
     light = _nfn(1, n_flows=2, hidden_sizes=(16, 16), noise_reg=("rule_of_thumb", 0.1), trainable_base_dist=True)
     light.fit(x, y, epochs=700, verbose=0)
     assert light.pdf(xt, yt).sum().item() / 700.0 > p1.sum() / 700.0
+
+
+def test_weight_gradients_fused_dense_match_autodiff_oracle(gpu):
+    """The same training loss through ops.log_prob_dense (output Dense layer fused into
+    the chain forward and backward, t never materialised) with H = 16: every MLP weight
+    gradient against fp64 autodiff of the oracle's op sequence."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d = ("planar", "radial", "radial"), 1
+    m = _nfn(d, flow_types=ft, hidden_sizes=(10, 16), trainable_base_dist=True, n_dims_x=1)
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((300, 1)).astype(np.float32)
+    y = (np.sin(2 * x) + 0.3 * rng.standard_normal((300, 1))).astype(np.float32)
+    m._mlp.to(gpu)
+    ws = [w.detach().requires_grad_(True) for w in m._mlp.weights + m._mlp.biases]
+    nw = len(m._mlp.weights)
+
+    def hidden(xx, params):
+        h = xx
+        for i in range(nw - 1):
+            h = torch.relu(h @ params[i] + params[nw + i])
+        return h
+
+    h = hidden(torch.from_numpy(x).to(gpu), ws)
+    loss = -ops.log_prob_dense(torch.from_numpy(y).to(gpu), h, ws[nw - 1], ws[2 * nw - 1], ft, d, True).mean()
+    loss.backward()
+    got = [w.grad.double().cpu() for w in ws]
+    ws64 = [w.detach().double().cpu().requires_grad_(True) for w in ws]
+    t64 = hidden(torch.from_numpy(x).double(), ws64) @ ws64[nw - 1] + ws64[2 * nw - 1]
+    lp64 = G.chain_log_prob_torch(torch.from_numpy(y).double(), t64, ft, d, True)
+    (-lp64.mean()).backward()
+    for g, w in zip(got, ws64):
+        torch.testing.assert_close(g, w.grad, rtol=2e-4, atol=2e-5)
+
+
+def test_fit_fused_dense_matches_unfused(gpu):
+    """fit with the fused Dense path (hidden width 16) and with the materialised t give
+    the same training trajectory up to fp32 rounding, and the fused model fits."""
+    rng = np.random.default_rng(22)
+    x, y = _sinusoid(400, rng)
+    losses = {}
+    for fused in (True, False):
+        m = _nfn(1, n_flows=3, hidden_sizes=(16, 16), trainable_base_dist=True)
+        m.fused_dense = fused
+        losses[fused] = m.fit(x, y, epochs=50, verbose=0)["loss"]
+    assert losses[True][-1] < losses[True][0]
+    np.testing.assert_allclose(losses[True][:10], losses[False][:10], rtol=1e-4)
+    np.testing.assert_allclose(losses[True][-1], losses[False][-1], rtol=2e-2)
