@@ -64,27 +64,48 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradAr
     for (int nt = 0; nt < NN; ++nt) dw[mh][nt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
   float db = 0.0f;  // lane p < P: column p of sum_b dt_b
 
+  // the next tile's h rows, y and upstream gradient are prefetched into registers
+  // (non-temporal) while the current tile runs; QH = H / 4 <= 4 * MH float4 per lane
+  const int r0 = lane / QH, c4 = lane - (lane / QH) * QH, rstep = 64 / QH;
+  float4 hbuf[4 * MH];
+  float ybuf[DM];
+  float gbuf = 1.0f;
+  auto issue = [&](int64_t tile) {
+    const int64_t b0 = tile * 64;
+    const int nr = (int)min((int64_t)64, a.B - b0);
+#pragma unroll
+    for (int k = 0; k < 4 * MH; ++k) {
+      const int r = r0 + k * rstep;
+      hbuf[k] = (k < QH && r < nr) ? load_row4<true>(da.h + (b0 + r) * hs + 4 * c4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int j = 0; j < DM; ++j) ybuf[j] = (lane < nr && j < d) ? a.y[(b0 + lane) * a.y_bstride + j] : 0.0f;
+    gbuf = (lane < nr && g.g_out) ? g.g_out[b0 + lane] : 1.0f;
+  };
+  if (u0 < a.ntiles) issue(u0);
   for (int64_t tile = u0; tile < a.ntiles; tile += ustep) {
     const int64_t b0 = tile * 64;
     const int nr = (int)min((int64_t)64, a.B - b0);
     // 1. h tile -> LDS (rows past B are zero: they add nothing to dW)
-    for (int i = lane; i < 64 * QH; i += 64) {
-      const int r = i / QH, c = i - (i / QH) * QH;
-      const float4 v = r < nr ? load_row4<true>(da.h + (b0 + r) * hs + 4 * c) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      float* dst = hl + r * SH + 4 * c;
-      dst[0] = v.x;
-      dst[1] = v.y;
-      dst[2] = v.z;
-      dst[3] = v.w;
+#pragma unroll
+    for (int k = 0; k < 4 * MH; ++k) {
+      if (k < QH) {
+        float* dst = hl + (r0 + k * rstep) * SH + 4 * c4;
+        dst[0] = hbuf[k].x;
+        dst[1] = hbuf[k].y;
+        dst[2] = hbuf[k].z;
+        dst[3] = hbuf[k].w;
+      }
     }
     float z[DM];
 #pragma unroll
     for (int j = 0; j < DM; ++j) {
-      z[j] = (lane < nr && j < d) ? a.y[(b0 + lane) * a.y_bstride + j] : 0.0f;
+      z[j] = ybuf[j];
       if (a.y_mean && j < d) z[j] = f_div<FAST>(z[j] - a.y_mean[j], a.y_std[j]);
     }
-    const float gl = (lane < nr && g.g_out) ? g.g_out[b0 + lane] : 1.0f;
+    const float gl = gbuf;
     wave_lds_sync();
+    if (tile + ustep < a.ntiles) issue(tile + ustep);
     // 2. t = h W + b
 #pragma unroll
     for (int nt = 0; nt < NN; ++nt) {
