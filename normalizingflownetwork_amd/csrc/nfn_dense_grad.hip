@@ -189,7 +189,16 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradAr
         }
       }
     }
-    if (lane < P) {
+    if (NN <= 2) {  // P <= 32: two lanes per column, 32 rows each, combined across the halves
+      const int p = lane & 31, r0h = (lane >> 5) * 32;
+      float cs = 0.0f;
+      if (p < P) {
+#pragma unroll 8
+        for (int r = 0; r < 32; ++r) cs += tl[(r0h + r) * S + p];
+      }
+      cs += __shfl_xor(cs, 32);
+      if (lane < P) db += cs;
+    } else if (lane < P) {
       float cs = 0.0f;
       for (int r = 0; r < 64; ++r) cs += tl[r * S + lane];
       db += cs;
