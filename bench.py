@@ -14,7 +14,10 @@ all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
 resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+                  [--mode forward|grad|dense|dense_grad]
+  N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
+  bench.py --gpus N), or plain `python bench.py --gpus N`, which starts that launcher as a
+  child process itself (before touching the GPU) and exits with its status.
 
 Prints ONE JSON line on rank 0.
 """
@@ -60,108 +63,125 @@ def algorithmic_bytes_grad(d: int, P: int, B: int) -> float:
     return float(B) * (8 * d + 8 * P + 4)
 
 
-def cpu_baseline_grad(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 16) -> dict:
-    """Reference-path stand-in for the backward: the oracle's torch fp32 autodiff through
-    the same eager op sequence (what Keras does when the reference trains), 1 thread."""
-    from oracle import nfn_grad_oracle as G
-
-    ft, d, _, _ = CONFIGS[cfg]
-    P = G.total_param_size(ft, d, True)
-    rng = np.random.default_rng(22)
-    y = rng.standard_normal((sample_rows, d)).astype(np.float32)
-    t = rng.standard_normal((sample_rows, P)).astype(np.float32)
-    g = np.full((sample_rows,), -1.0 / sample_rows, np.float32)
-    nth = torch.get_num_threads()
-    torch.set_num_threads(1)
+def cpu_model() -> str:
     try:
-        run = lambda: G.chain_log_prob_grad(y, t, ft, d, True, g_out=g, dtype=np.float32)  # noqa: E731
-        run()
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            run()
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= seconds or reps >= 50:
-                break
-    finally:
-        torch.set_num_threads(nth)
-    return {
-        "value": reps * sample_rows / el,
-        "unit": "evals/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{sample_rows} samples of {cfg}, torch fp32 autodiff of the eager op sequence "
-                  f"(oracle/nfn_grad_oracle.py), {reps} reps in {el:.1f}s, 1 thread",
-    }
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def cpu_baseline_dense(cfg: str, H: int, seconds: float = 12.0, sample_rows: int = 1 << 20) -> dict:
-    """Reference-path stand-in for --mode dense: numpy fp32 t = h W + b (one BLAS GEMM,
-    as Keras' Dense) followed by the op-by-op chain restatement, 1 thread."""
+def cpu_workers() -> int:
+    """Host cores this process may use: its affinity mask, bounded by the job's thread
+    share (OMP_NUM_THREADS is the box's CPU share on the GPU pool, 16 per GPU)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def _cpu_job(kind: str, cfg: str, rows: int, seed: int, H: int):
+    """(run, evals per run) for one CPU-baseline worker: the oracle's op-by-op restatement of
+    the reference's eager path on `rows` samples (test infrastructure, timed only here)."""
     from oracle import nfn_oracle as O
 
     ft, d, _, S = CONFIGS[cfg]
     P = O.total_param_size(ft, d, True)
-    rng = np.random.default_rng(22)
-    rows = sample_rows if S is None else max(1, sample_rows // S)
-    lead = () if S is None else (S,)
+    rng = np.random.default_rng(seed)
     y = rng.standard_normal((rows, d)).astype(np.float32)
+    if kind == "forward":
+        if S is None:
+            t = rng.standard_normal((rows, P)).astype(np.float32)
+            return (lambda: O.chain_log_prob(y, t, ft, d, True, np.float32)), rows
+        t = rng.standard_normal((S, rows, P)).astype(np.float32)
+        return (lambda: O.posterior_lse(y, t, ft, d, True, dtype=np.float32)), rows * S
+    if kind == "grad":
+        from oracle import nfn_grad_oracle as G
+
+        t = rng.standard_normal((rows, P)).astype(np.float32)
+        g = np.full((rows,), -1.0 / rows, np.float32)
+        return (lambda: G.chain_log_prob_grad(y, t, ft, d, True, g_out=g, dtype=np.float32)), rows
+    lead = () if S is None else (S,)
     h = rng.standard_normal(lead + (rows, H)).astype(np.float32)
     W = (rng.standard_normal(lead + (H, P)) / np.sqrt(H)).astype(np.float32)
     b = (0.1 * rng.standard_normal(lead + (P,))).astype(np.float32)
-    if S is None:
-        run = lambda: O.chain_log_prob(y, h @ W + b, ft, d, True, np.float32)  # noqa: E731
-    else:  # the posterior over S draws of the output DenseVariational layer
-        run = lambda: O.posterior_lse(y, np.matmul(h, W) + b[:, None], ft, d, True, dtype=np.float32)  # noqa: E731
-    sample_rows = rows * (1 if S is None else S)
+    if kind == "dense":
+        if S is None:
+            return (lambda: O.chain_log_prob(y, h @ W + b, ft, d, True, np.float32)), rows
+        return (lambda: O.posterior_lse(y, np.matmul(h, W) + b[:, None], ft, d, True, dtype=np.float32)), rows * S
+    # dense_grad: Keras autodiff through Dense(P) and the chain = t by GEMM, the chain's
+    # autodiff (torch fp32 over the eager op sequence), then dh = dt W^T, dW = h^T dt, db
+    from oracle import nfn_grad_oracle as G
+
+    g = np.full((rows,), -1.0 / rows, np.float32)
+
+    def run():
+        t = h @ W + b
+        _, gt, gy = G.chain_log_prob_grad(y, t, ft, d, True, g_out=g, dtype=np.float32)
+        return gt @ W.T, h.T @ gt, gt.sum(0), gy
+
+    return run, rows
+
+
+def _cpu_worker(job):
+    """One process of the pooled baseline: single-threaded numerics on its own row slice,
+    timed until `seconds` have passed; returns (evals, elapsed)."""
+    kind, cfg, rows, seed, H, seconds = job
     from threadpoolctl import threadpool_limits
 
-    with threadpool_limits(limits=1):  # one BLAS thread: the baseline is single-core
-        run()
+    torch.set_num_threads(1)
+    with threadpool_limits(limits=1):
+        run, per = _cpu_job(kind, cfg, rows, seed, H)
+        run()  # warm
         reps, t0 = 0, time.perf_counter()
         while True:
             run()
             reps += 1
             el = time.perf_counter() - t0
-            if el >= seconds or reps >= 50:
+            if el >= seconds or reps >= 200:
                 break
-    return {"value": reps * sample_rows / el, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": f"{sample_rows} {'samples' if S is None else '(draw, sample) pairs'} of {cfg} with H={H}: numpy fp32 GEMM + op-by-op chain "
-                      f"(oracle/nfn_oracle.py), {reps} reps in {el:.1f}s"}
+    return reps * per, el
 
 
-def cpu_baseline(cfg: str, seconds: float = 12.0, sample_rows: int = 1 << 20) -> dict:
-    """The reference-path stand-in timed on this host: the oracle's fp32 op-by-op
-    numpy restatement (whole-batch ops, TF-eager op order) on a bounded slice."""
-    from oracle import nfn_oracle as O
+def cpu_baseline(kind: str, cfg: str, H: int = 16, seconds: float = 8.0) -> dict:
+    """The reference-path stand-in timed on this host's cores (rank 0, N = 1 only): the
+    oracle's fp32 op-by-op restatement of TF eager's per-op evaluation
+    (`BaseEstimator.py:77-86` / `:19-31` for the backward).  TF runs each Eigen op over its
+    intra-op pool on every core, so the headline `value` splits a bounded batch into one
+    row slice per core and runs them concurrently in a process pool (one BLAS / torch
+    thread each); `single_thread` is the same restatement on one core."""
+    import multiprocessing as mp
 
     ft, d, _, S = CONFIGS[cfg]
-    rows = sample_rows if S is None else max(1, sample_rows // S)
-    P = O.total_param_size(ft, d, True)
-    rng = np.random.default_rng(22)
-    y = rng.standard_normal((rows, d)).astype(np.float32)
-    if S is None:
-        t = rng.standard_normal((rows, P)).astype(np.float32)
-        run = lambda: O.chain_log_prob(y, t, ft, d, True, np.float32)  # noqa: E731
-    else:
-        t = rng.standard_normal((S, rows, P)).astype(np.float32)
-        run = lambda: O.posterior_lse(y, t, ft, d, True, dtype=np.float32)  # noqa: E731
-    run()  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 50:
-            break
-    evals = reps * rows * (1 if S is None else S)
+    total = {"forward": 1 << 20, "dense": 1 << 20, "grad": 1 << 16, "dense_grad": 1 << 16}[kind]
+    if S is not None:
+        total = max(64, total // S)
+    n = cpu_workers()
+    one_evals, one_el = _cpu_worker((kind, cfg, total, 22, H, seconds))
+    rows = max(64, total // n)
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's HIP state is inherited
+    with ctx.Pool(n) as pool:
+        res = pool.map(_cpu_worker, [(kind, cfg, rows, 22 + i, H, seconds) for i in range(n)])
+    pooled = sum(e / el for e, el in res)
+    unit_rows = "(draw, sample) pairs" if S is not None else "samples"
+    what = {"forward": "numpy fp32 op-by-op chain", "dense": "numpy fp32 GEMM + op-by-op chain",
+            "grad": "torch fp32 autodiff of the eager op sequence",
+            "dense_grad": "numpy GEMM + torch fp32 autodiff of the eager op sequence + weight-gradient GEMMs"}[kind]
     return {
-        "value": evals / el,
+        "value": pooled,
         "unit": "evals/s",
-        "cores": 1,
+        "cores": n,
         "kind": "port",
-        "sample": f"{rows} samples{'' if S is None else f' x {S} draws'} of {cfg}, numpy fp32 op-by-op restatement "
-                  f"of the TF eager path (oracle/nfn_oracle.py), {reps} reps in {el:.1f}s, 1 thread",
+        "sample": f"{cfg} {kind}: {n} concurrent single-threaded workers x {rows} rows (a {rows * n}-row batch "
+                  f"split per core, as TF's intra-op pool splits each op), {what} (oracle/), ~{seconds:.0f} s each",
+        "single_thread": one_evals / one_el,
+        "single_thread_sample": f"{total} rows on 1 core ({unit_rows})",
+        "host_cpus": os.cpu_count(),
+        "cpu_model": cpu_model(),
     }
 
 
@@ -180,6 +200,35 @@ def load_traffic(cfg: str, B: int):
     return float(rec["hbm_bytes_per_launch"]), os.path.relpath(cands[-1], REPO)
 
 
+def spawn_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: run N ranks as a CHILD
+    `torch.distributed.run` (one process per GPU, 127.0.0.1 rendezvous) with the same
+    arguments, stream its output and return its exit code.  Runs before anything here
+    touches the GPU; nothing is exec'd in place."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def nfn_environment() -> dict:
+    """Every NFN_* variable in the environment (recorded in the JSON line).  The release
+    library reads only NFN_MATH (overridden by --math); the tuning / ablation knobs exist
+    only in the NFN_DIAG build, and an ablation knob in the environment aborts the bench."""
+    env = {k: v for k, v in os.environ.items() if k.startswith("NFN_")}
+    bad = [k for k in env if k.startswith("NFN_ABLATE")]
+    if bad:
+        raise SystemExit(f"refusing to benchmark with ablation knobs set: {bad}")
+    return env
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,21 +241,25 @@ def main():
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="override the per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
-    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad"],
                     help="forward = fused log_prob (the headline); grad = the fused backward of the "
                          "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient); dense = the "
-                         "output Dense layer (H -> P) fused into the chain, streaming h instead of t")
-    ap.add_argument("--hidden", type=int, default=16, help="--mode dense: hidden width H")
+                         "output Dense layer (H -> P) fused into the chain, streaming h instead of t; "
+                         "dense_grad = the training step's backward through that fused layer (dh, dW, db, dy)")
+    ap.add_argument("--hidden", type=int, default=16, help="--mode dense / dense_grad: hidden width H")
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the all-reduce even at N = 1 (tests)")
     ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
                     help="N > 1 mean all-reduce: torch.distributed, or the library's own RCCL "
                          "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
     args = ap.parse_args()
+    nfn_env = nfn_environment()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
 
     rank, world, local_rank = init_from_env(backend=args.backend, force=args.force_pg)
     dist_on = dist.is_initialized()  # world > 1, or --force-pg (test hook: the N > 1 step path at N = 1)
@@ -216,6 +269,11 @@ def main():
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     ops.set_math_mode(args.math)
+    pg_world = dist.get_world_size() if dist_on else 1
+    rank_devices = [dev_index]
+    if dist_on:
+        rank_devices = [None] * pg_world
+        dist.all_gather_object(rank_devices, dev_index)
 
     ft, d, B, S = CONFIGS[args.config]
     if args.batch:
@@ -223,34 +281,39 @@ def main():
     P = ops.total_param_size(ft, d, True)
     gen = torch.Generator(device=dev).manual_seed(22 + rank)
     y = torch.randn((B, d), generator=gen, device=dev)
-    t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
-    grad_mode = args.mode == "grad"
-    dense_mode = args.mode == "dense"
+    grad_mode = args.mode in ("grad", "dense_grad")
+    dense_mode = args.mode in ("dense", "dense_grad")
+    H = args.hidden
     if dense_mode:
-        # C5: the posterior with the output DenseVariational layer fused (per draw h_s, W_s, b_s)
-        H = args.hidden
-        del t
+        # the output Dense layer fused: per sample h (B, H) instead of t (B, P); C5: the
+        # posterior with the output DenseVariational layer fused (per draw h_s, W_s, b_s)
         hgen = torch.Generator(device=dev).manual_seed(122 + rank)
         lead = () if S is None else (S,)
         h = torch.randn(lead + (B, H), generator=hgen, device=dev)
         Wd = torch.randn(lead + (H, P), generator=hgen, device=dev) / float(np.sqrt(H))
         bd = 0.1 * torch.randn(lead + (P,), generator=hgen, device=dev)
-        launcher = (ops.DenseLauncher if S is None else ops.PosteriorDenseLauncher)(y, h, Wd, bd, ft, d, True)
-    elif grad_mode:
-        assert S is None, "--mode grad covers the plain chain configs (C2, C3)"
-        g_up = torch.full((B,), -1.0 / B, dtype=torch.float32, device=dev)  # d(mean NLL)/d log_prob
-        launcher = ops.GradLauncher(y, t, ft, d, True, g_out=g_up)
+        if grad_mode:
+            assert S is None, "--mode dense_grad covers the plain chain configs (C2, C3)"
+            g_up = torch.full((B,), -1.0 / B, dtype=torch.float32, device=dev)  # d(mean NLL)/d log_prob
+            launcher = ops.DenseGradLauncher(y, h, Wd, bd, ft, d, True, g_out=g_up)
+        else:
+            launcher = (ops.DenseLauncher if S is None else ops.PosteriorDenseLauncher)(y, h, Wd, bd, ft, d, True)
     else:
-        launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
+        t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
+        if grad_mode:
+            assert S is None, "--mode grad covers the plain chain configs (C2, C3)"
+            g_up = torch.full((B,), -1.0 / B, dtype=torch.float32, device=dev)  # d(mean NLL)/d log_prob
+            launcher = ops.GradLauncher(y, t, ft, d, True, g_out=g_up)
+        else:
+            launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
-    # (sum, count) all-reduce buffers: a ring of two, so step i's all-reduce (async, on
-    # the process group's stream) overlaps step i+1's chain kernel; a buffer is reused
-    # only after the stream has waited for its previous all-reduce
-    reds = [torch.zeros((2,), dtype=torch.float64, device=dev) for _ in range(2)]
+    # (sum, count, non-finite) all-reduce buffers: a ring of two, so step i's all-reduce
+    # (async, on the process group's stream) overlaps step i+1's chain kernel; a buffer
+    # is reused only after the stream has waited for its previous all-reduce
+    reds = [torch.zeros((3,), dtype=torch.float64, device=dev) for _ in range(2)]
     works = [None, None]
     nstep = [0]
-    red = reds[0]
     evals_per_step = B * (1 if S is None else S)
     native = None
     if dist_on and args.allreduce == "native":
@@ -268,24 +331,25 @@ def main():
             return
         s = launcher.finish_sum(sh)
         if native is not None:
-            native.allreduce_mean(s, B, sh)
+            native.allreduce_mean(s, B, sh, local_nonfinite=launcher.nonfinite)
         elif dist_on:
             i = nstep[0] % 2
             nstep[0] += 1
+            buf = reds[i]
             if args.backend == "nccl":
                 if works[i] is not None:
                     works[i].wait()  # stream-side wait: the buffer's previous all-reduce is done
-                buf = reds[i]
                 buf[0:1].copy_(s)
                 buf[1] = float(B)
+                buf[2:3].copy_(launcher.nonfinite)
                 works[i] = dist.all_reduce(buf, async_op=True)
             else:  # gloo reduces host tensors
-                buf = reds[i]
                 buf[0:1].copy_(s)
                 buf[1] = float(B)
-                h = buf.cpu()
-                dist.all_reduce(h)
-                buf.copy_(h)
+                buf[2:3].copy_(launcher.nonfinite)
+                hb = buf.cpu()
+                dist.all_reduce(hb)
+                buf.copy_(hb)
             last_red[0] = buf
 
     last_red = [reds[0]]
@@ -342,73 +406,90 @@ def main():
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
     unfused_ms = None
-    if dense_mode and rank == 0:
+    if args.mode == "dense" and rank == 0:
         # the same x->density work unfused: t = h W + b by the library GEMM (t written to
         # HBM), then the chain kernel over t (read back) — what the fusion replaces
         t_buf = torch.empty((B, P) if S is None else (S, B, P), dtype=torch.float32, device=dev)
         plain = ops.ChainLauncher(y, t_buf, ft, d, True, write_values=True, draws=S)
 
-        def gemm():
+        def unfused():
             if S is None:
                 torch.addmm(bd, h, Wd, out=t_buf)
             else:
                 torch.baddbmm(bd[:, None, :], h, Wd, out=t_buf)
-
-        for _ in range(3):
-            gemm()
             plain.launch(sh)
+    elif args.mode == "dense_grad" and rank == 0:
+        # unfused: t by the library GEMM, the chain backward kernel, library GEMMs for dh / dW, db
+        t_buf = torch.empty((B, P), dtype=torch.float32, device=dev)
+        plain = ops.GradLauncher(y, t_buf, ft, d, True, g_out=g_up)
+
+        def unfused():
+            torch.addmm(bd, h, Wd, out=t_buf)
+            plain.launch(sh)
+            gt = plain.grad_t
+            return gt @ Wd.t(), h.t() @ gt, gt.sum(0)
+    if dense_mode and rank == 0:
+        for _ in range(3):
+            unfused()
         pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
         for e0, e1 in pairs:
             e0.record(stream)
-            gemm()
-            plain.launch(sh)
+            unfused()
             e1.record(stream)
         torch.cuda.synchronize()
         unfused_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in pairs]))
         del t_buf, plain
+    nonfinite = None
     if grad_mode:
         mean_ll = None
     elif native is not None:
         mean_ll = float(native.mean.item())
-    else:
+        nonfinite = int(native.sum_count[2].item())
+    elif dist_on:
         red = last_red[0]
-        mean_ll = float(red[0].item() / red[1].item()) if dist_on else float(launcher.sum.item()) / B
+        mean_ll = float(red[0].item() / red[1].item())
+        nonfinite = int(red[2].item())
+    else:
+        mean_ll = float(launcher.sum.item()) / B
+        nonfinite = int(launcher.nonfinite.item())
 
     if rank == 0:
         total_evals = evals_per_step * world * args.steps
         value = total_evals / elapsed
-        if grad_mode:
+        if args.mode == "grad":
             bytes_launch = algorithmic_bytes_grad(d, P, B)
-        elif dense_mode:
+        elif args.mode == "dense":
             nd = 1 if S is None else S
-            bytes_launch = float(B) * (4 * args.hidden * nd + 4 * d + 4) + nd * (4.0 * args.hidden * P + 4.0 * P)
+            bytes_launch = float(B) * (4 * H * nd + 4 * d + 4) + nd * (4.0 * H * P + 4.0 * P)
+        elif args.mode == "dense_grad":
+            # h, y, upstream g in; dh, dy out; W, b read and dW, db written once per launch
+            bytes_launch = float(B) * (8 * H + 8 * d + 4) + 2 * (4.0 * H * P + 4.0 * P)
         else:
             bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense"}.get(args.mode, ""), B)
+        traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense",
+                                                           "dense_grad": "_dense_grad"}.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            if grad_mode:
-                cpu = cpu_baseline_grad(args.config, seconds=args.cpu_seconds)
-            elif dense_mode:
-                cpu = cpu_baseline_dense(args.config, args.hidden, seconds=args.cpu_seconds)
-            else:
-                cpu = cpu_baseline(args.config, seconds=args.cpu_seconds)
+            cpu = cpu_baseline(args.mode, args.config, H=H, seconds=args.cpu_seconds)
         wl = {
             "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
             "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
             "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
         }[args.config]
-        if grad_mode:
+        if args.mode == "grad":
             kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group1_kernel"
             metric = f"log_prob backward evals/sec (whole node), {args.config}"
-        elif dense_mode:
+        elif args.mode == "dense_grad":
+            kernel_name = "chain_dense_grad_kernel + sum_partials_kernel"
+            metric = f"Dense(H={H})->log_prob backward evals/sec (whole node), {args.config}"
+        elif args.mode == "dense":
             if S is None:
                 kernel_name = "chain_dense1_kernel" if d == 1 else "chain_dense_kernel"
-                metric = f"Dense(H={args.hidden})->log_prob evals/sec (whole node), {args.config}"
+                metric = f"Dense(H={H})->log_prob evals/sec (whole node), {args.config}"
             else:
                 kernel_name = "posterior_dense1_kernel" if d == 1 else "posterior_dense_kernel"
-                metric = f"DenseVariational(H={args.hidden})->posterior (draw, sample) evals/sec (whole node), {args.config}"
+                metric = f"DenseVariational(H={H})->posterior (draw, sample) evals/sec (whole node), {args.config}"
         else:
             kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel",
                            "C5": "chain_persistent_kernel + posterior_merge_kernel"}[args.config]
@@ -419,6 +500,8 @@ def main():
             "value": value,
             "unit": "evals/s",
             "n_gpus": world,
+            "pg_world_size": pg_world,
+            "rank_devices": rank_devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
@@ -436,6 +519,7 @@ def main():
                 "y_dim": d,
                 "flows": list(ft),
                 "param_width": P,
+                "hidden": H if dense_mode else None,
                 "trainable_base": True,
                 "math": args.math,
                 "parallelism": f"dp{world}",
@@ -456,7 +540,9 @@ def main():
             },
             "cpu_baseline": cpu,
             "mean_log_prob": mean_ll,
-            "unfused_gemm_plus_chain_ms": unfused_ms,
+            "nonfinite_log_prob": nonfinite,
+            "unfused_ms": unfused_ms,
+            "nfn_env": nfn_env,
         }
         print(json.dumps(line), flush=True)
     if native is not None:

@@ -112,7 +112,7 @@ int32_t nfn_param_size(int32_t flow_id, int32_t d);
 int32_t nfn_total_param_size(const int32_t* flow_ids, int32_t K, int32_t d, int32_t trainable_base);
 
 /* Number of doubles of device workspace nfn_chain_logprob_f32 needs when
- * out_sum != NULL (per-workgroup partial sums). */
+ * out_sum != NULL (per-workgroup partial sums and non-finite counts). */
 int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
 
 /*
@@ -123,12 +123,16 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *   t          : (B or 1, P) rows at t_rowstride floats (0 = broadcast), P = nfn_total_param_size
  *   y_mean/y_std : (d,) device arrays or both NULL
  *   out_logp   : (B,) may be NULL when only the sum is wanted
- *   out_sum    : device double[1] or NULL — receives sum_b out_logp[b] (fp64 accumulation)
+ *   out_sum    : device double[1] or NULL — receives sum_b out_logp[b] (fp64 accumulation;
+ *                non-finite values propagate, as in the reference's .mean())
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
- *                Layout: workspace[0] = number n of partial sums written,
- *                workspace[1 .. n] = per-workgroup fp64 partial sums.  With
- *                out_sum == NULL and workspace != NULL only the partials are written
- *                (finish with nfn_reduce_partials_f64).
+ *                Layout: workspace[0] = number n of per-workgroup pairs written,
+ *                workspace[1] = number of non-finite out_logp values (written by the
+ *                reduction, i.e. valid once out_sum is), workspace[2 + 2i] /
+ *                workspace[3 + 2i] = workgroup i's fp64 partial sum / non-finite count.
+ *                With out_sum == NULL and workspace != NULL only the pairs are written
+ *                (finish with nfn_reduce_partials_f64).  One workspace per call in
+ *                flight: two calls sharing one race.
  */
 int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
                               int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
@@ -203,9 +207,11 @@ int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride,
  * (deterministic). */
 int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream);
 
-/* out[0] = sum of the partials a chain / posterior call left in `workspace`
- * (workspace[0] = count, workspace[1..count]); finishes a partials-only call. */
-int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream);
+/* Finishes a partials-only call: out_sum[0] = sum of the partial sums a chain /
+ * posterior call left in `workspace`; the total non-finite count goes to workspace[1]
+ * and, if out_nonfinite != NULL, to out_nonfinite[0] (a device double).  Fixed order:
+ * bitwise deterministic. */
+int32_t nfn_reduce_partials_f64(double* workspace, double* out_sum, double* out_nonfinite, void* stream);
 
 /* Number of doubles of device workspace for nfn_posterior_lse_f32: the partials
  * block (as for the chain) followed by the draw-split region.  Passing a
@@ -270,15 +276,16 @@ int32_t nfn_posterior_lse_dense_f32(const float* y, int64_t y_bstride, const flo
  *   nfn_comm_unique_id : rank 0 creates the 128-byte rendezvous id, which the
  *                        caller distributes to every rank (any channel).
  *   nfn_comm_init      : collective over all ranks; binds the CURRENT HIP device.
- *   nfn_allreduce_mean : sum_count (device double[2]) := sum over ranks of
- *                        {local_sum[0], local_count}; mean_out (device double[1],
- *                        nullable) := sum / count.  Stream-ordered, no host sync.
+ *   nfn_allreduce_mean : sum_count (device double[3]) := sum over ranks of
+ *                        {local_sum[0], local_count, local_nonfinite[0] (0 if NULL)};
+ *                        mean_out (device double[1], nullable) := sum / count.
+ *                        One 24-byte RCCL all-reduce.  Stream-ordered, no host sync.
  */
 int32_t nfn_comm_unique_id(uint8_t* id_out);
 int32_t nfn_comm_init(void** comm_out, int32_t nranks, const uint8_t* id, int32_t rank);
 int32_t nfn_comm_destroy(void* comm);
-int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, double* sum_count,
-                           double* mean_out, void* stream);
+int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, const double* local_nonfinite,
+                           double* sum_count, double* mean_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@ import os
 
 LIB_NAME = "libnfn_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+DIAG_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnfn_hip_diag.so")
 
 # Symbols declared in include/nfn.h, with their ctypes signatures.
 _c_int32 = ctypes.c_int32
@@ -23,7 +24,7 @@ SIGNATURES = {
     "nfn_last_error": (ctypes.c_char_p, []),
     "nfn_set_math_mode": (_c_int32, [_c_int32]),
     "nfn_reduce_sum_f64": (_c_int32, [_vp, _c_int64, _vp, _vp]),
-    "nfn_reduce_partials_f64": (_c_int32, [_vp, _vp, _vp]),
+    "nfn_reduce_partials_f64": (_c_int32, [_vp, _vp, _vp, _vp]),
     "nfn_param_size": (_c_int32, [_c_int32, _c_int32]),
     "nfn_total_param_size": (_c_int32, [_vp, _c_int32, _c_int32, _c_int32]),
     "nfn_chain_workspace_doubles": (_c_int64, [_c_int64, _c_int32, _c_int32]),
@@ -76,7 +77,7 @@ SIGNATURES = {
     "nfn_comm_unique_id": (_c_int32, [_vp]),
     "nfn_comm_init": (_c_int32, [ctypes.POINTER(_vp), _c_int32, _vp, _c_int32]),
     "nfn_comm_destroy": (_c_int32, [_vp]),
-    "nfn_allreduce_mean": (_c_int32, [_vp, _vp, _c_int64, _vp, _vp, _vp]),
+    "nfn_allreduce_mean": (_c_int32, [_vp, _vp, _c_int64, _vp, _vp, _vp, _vp]),
 }
 
 # Status codes (include/nfn.h)
@@ -108,6 +109,15 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def use_diagnostic_build() -> None:
+    """Bind ``libnfn_hip_diag.so`` (built with ``-DNFN_DIAG``: tuning / ablation knobs read
+    from ``NFN_*`` environment variables) instead of the release library.  For
+    ``tools/microbench.py`` only; must run before the first :func:`load`."""
+    global LIB_PATH, LIB_NAME
+    assert _lib is None, "the release library is already loaded"
+    LIB_PATH, LIB_NAME = DIAG_LIB_PATH, os.path.basename(DIAG_LIB_PATH)
 
 
 def last_error() -> str:

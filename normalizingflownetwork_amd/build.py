@@ -2,7 +2,12 @@
 
 The kernels are split over several translation units (fast / precise math
 instantiations compile as separate objects) that are compiled in parallel and
-linked into one shared library."""
+linked into one shared library.
+
+``--diag`` (``build(diag=True)``) builds ``libnfn_hip_diag.so`` with ``-DNFN_DIAG``:
+the same kernels plus the tuning / ablation knobs read from ``NFN_*`` environment
+variables, for ``tools/microbench.py`` only.  The release library reads none of them
+(only ``NFN_MATH``, the documented initial math mode)."""
 
 from __future__ import annotations
 
@@ -17,6 +22,8 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 OBJ_DIR = os.path.join(PKG_DIR, "_obj")
 OUT = os.path.join(PKG_DIR, "libnfn_hip.so")
+DIAG_OBJ_DIR = os.path.join(PKG_DIR, "_obj_diag")
+DIAG_OUT = os.path.join(PKG_DIR, "libnfn_hip_diag.so")
 ARCH = os.environ.get("NFN_OFFLOAD_ARCH", "gfx950")
 HEADERS = [os.path.join(CSRC, "nfn_device.h"), os.path.join(CSRC, "nfn_launch.h"),
            os.path.join(CSRC, "nfn_grad_device.h"),
@@ -62,12 +69,12 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(unit, verbose: bool) -> str:
+def _compile(unit, verbose: bool, obj_dir: str, extra) -> str:
     name, src, flags = unit
-    obj = os.path.join(OBJ_DIR, name + ".o")
+    obj = os.path.join(obj_dir, name + ".o")
     srcp = os.path.join(CSRC, src)
     if _stale(obj, [srcp] + HEADERS):
-        cmd = [hipcc()] + _common() + flags + ["-c", srcp, "-o", obj + ".tmp"]
+        cmd = [hipcc()] + _common() + list(extra) + flags + ["-c", srcp, "-o", obj + ".tmp"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -75,25 +82,26 @@ def _compile(unit, verbose: bool) -> str:
     return obj
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
+def build(force: bool = False, verbose: bool = True, jobs: int = 0, diag: bool = False) -> str:
     """Compile (in parallel) the translation units that are out of date and link."""
-    os.makedirs(OBJ_DIR, exist_ok=True)
+    obj_dir, out, extra = (DIAG_OBJ_DIR, DIAG_OUT, ["-DNFN_DIAG"]) if diag else (OBJ_DIR, OUT, [])
+    os.makedirs(obj_dir, exist_ok=True)
     if force:
         for u in UNITS:
-            p = os.path.join(OBJ_DIR, u[0] + ".o")
+            p = os.path.join(obj_dir, u[0] + ".o")
             if os.path.exists(p):
                 os.remove(p)
     jobs = jobs or min(len(UNITS), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda u: _compile(u, verbose), UNITS))
-    if force or _stale(OUT, objs):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs + LINK_LIBS
+        objs = list(ex.map(lambda u: _compile(u, verbose, obj_dir, extra), UNITS))
+    if force or _stale(out, objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs + LINK_LIBS
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-        os.replace(OUT + ".tmp", OUT)
-    return OUT
+        os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, diag="--diag" in sys.argv)

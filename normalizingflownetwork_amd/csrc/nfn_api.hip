@@ -83,10 +83,12 @@ TileGeom tile_geom(int P) {
   g.lds_stride = P | 1;  // odd stride: conflict-free per-lane ds_read_b32
   const size_t row_bytes = (size_t)g.lds_stride * sizeof(float);
   int rows = kMaxBlock;
+#ifdef NFN_DIAG
   if (const char* e = getenv("NFN_TILE_ROWS")) {  // tuning knob: 64, 128, 192 or 256
     const int r = atoi(e);
     if (r >= 64 && r <= kMaxBlock && r % 64 == 0) rows = r;
   }
+#endif
   while (rows > 64 && (size_t)rows * row_bytes > (size_t)kLdsTileBudget) rows -= 64;
   // very wide rows (up to NFN_MAX_FLOWS x (2 NFN_MAX_DIMS + 1) floats): fewer samples
   // per tile so the tile fits the 160 KiB of LDS a workgroup may hold
@@ -102,6 +104,9 @@ TileGeom tile_geom(int P) {
 enum LoadMode { kAuto = 0, kCoop = 1, kOwnRow = 2, kTile = 3, kWave = 4 };
 
 int load_mode_env() {
+#ifndef NFN_DIAG
+  return kAuto;  // release build: the measured default only
+#endif
   const char* e = getenv("NFN_LOAD_MODE");
   if (!e) return kAuto;
   if (!strcmp(e, "coop")) return kCoop;
@@ -132,21 +137,26 @@ void group_shape(int dm, int want_g, int* G, int* DPL) {
     if (x.dm == dm && x.g == want_g) { *G = x.g; *DPL = x.dpl; }
 }
 
-// One fp64 partial per workgroup at the smallest tile (64 rows).
+// Number of (sum, non-finite count) partial pairs the workspace holds: one per
+// workgroup of the smallest tile any launch uses (64 rows, fewer for very wide
+// rows).  Persistent launches whose grid could exceed it are capped at it
+// (ChainArgs::grid_cap), so no launch writes past the workspace.
 int64_t partials_capacity(int64_t B, int P) {
   const int rows = std::min(64, tile_geom(P < 0 ? 0 : P).rows);
   return (B + rows - 1) / rows;
 }
 
-// Draw ranges per tile for the posterior: enough (tile, range) units for every
-// resident team (~2 per team: 8 workgroups of 256 rows, or 32 waves of 64 rows,
-// per CU on a 256-CU MI355X), at most 16 ranges.  Both targets give the same
-// split for a given B, so the workspace size does not depend on the mode.
-int posterior_split(int64_t B, int rows) {
-  const int64_t target = rows >= 256 ? 2048 : 2048 * (256 / rows);
-  const int64_t ntiles = (B + rows - 1) / rows;
+// Doubles of the [count | non-finite | (sum, count) pairs] block.
+int64_t partials_doubles(int64_t B, int P) { return 2 + 2 * partials_capacity(B, P); }
+
+// Draw ranges per tile for the posterior: enough (64-row tile, range) units for
+// ~2 per resident wave (32 waves per CU on a 256-CU MI355X), at most 16 ranges.
+// ONE function sizes the workspace's split region and bounds every launch's split.
+int posterior_split(int64_t B) {
+  constexpr int64_t kTarget = 2048 * 4;
+  const int64_t ntiles = (B + 63) / 64;
   if (ntiles <= 0) return 1;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (target + ntiles - 1) / ntiles));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(16, (kTarget + ntiles - 1) / ntiles));
 }
 
 int32_t check_hip(const char* what) {
@@ -166,7 +176,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   if (P < 0) return P;
   // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
   // the flow math, to measure the memory path of the kernel structure alone.
-  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // NFN_DIAG builds only (env_int)
   a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
   a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
@@ -194,7 +204,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   a.y_mean = y_mean;
   a.y_std = y_std;
   a.out = out;
-  a.partials = workspace ? workspace + 1 : nullptr;  // workspace[0] = number of partials
+  a.partials = workspace ? workspace + 2 : nullptr;  // [count | non-finite | pairs]
+  a.grid_cap = workspace ? partials_capacity(B, P) : 0;
   a.y_bstride = y_bstride;
   a.t_rowstride = t_rowstride;
   a.t_drawstride = t_drawstride;
@@ -251,20 +262,21 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     if (posterior) {
       // draw split: more (tile, draw-range) units when the batch alone is too small
       // to fill the chip; needs the split region of the workspace
-      int nsplit = workspace ? std::min(posterior_split(B, tile_rows), S) : 1;
-      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(std::min(env_int("NFN_POST_SPLIT", 1), S),
-                                                             workspace ? posterior_split(B, g.rows) : 1);
+      // (the split region holds posterior_split(B) ranges; never more are used)
+      int nsplit = workspace ? std::min(posterior_split(B), S) : 1;
+      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(env_int("NFN_POST_SPLIT", 1), nsplit);
       a.nsplit = nsplit;
       a.dps = (S + nsplit - 1) / nsplit;
-      a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges
-      a.split_out = reinterpret_cast<float2*>(workspace + 1 + partials_capacity(B, P));
+      a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges (<= nsplit)
+      a.split_out = reinterpret_cast<float2*>(workspace + partials_doubles(B, P));
+      if (a.nsplit > 1) a.grid_cap = 0;  // partials come from the merge kernel
       if (fast) launch_persistent_fast(true, dm, Q, a, g.rows, lds_p, s, &nblk);
       else launch_persistent_precise(true, dm, Q, a, g.rows, lds_p, s, &nblk);
       if (a.nsplit > 1) {
         int32_t rc0 = check_hip("posterior kernel launch");
         if (rc0 != NFN_OK) return rc0;
         nblk = (B + kMaxBlock - 1) / kMaxBlock;
-        launch_posterior_merge(fast, (const float2*)a.split_out, a.nsplit, S, B, out, workspace + 1, s);
+        launch_posterior_merge(fast, (const float2*)a.split_out, a.nsplit, S, B, out, workspace ? workspace + 2 : nullptr, s);
       }
     } else {
       if (fast) launch_persistent_fast(false, dm, Q, a, g.rows, lds_p, s, &nblk);
@@ -280,7 +292,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
   if (rc != NFN_OK) return rc;
   if (out_sum) {
-    launch_reduce_partials((const double*)workspace, out_sum, s);
+    launch_reduce_partials(workspace, out_sum, nullptr, s);
     rc = check_hip("reduce_partials_kernel launch");
   }
   return rc;
@@ -410,7 +422,7 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   a.y_mean = y_mean;
   a.y_std = y_std;
   a.out = out;
-  a.partials = workspace ? workspace + 1 : nullptr;
+  a.partials = workspace ? workspace + 2 : nullptr;
   a.y_bstride = y_bstride;
   a.B = B;
   a.d = d;
@@ -435,7 +447,7 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   int32_t rc = check_hip("chain_dense_kernel launch");
   if (rc != NFN_OK) return rc;
   if (out_sum) {
-    launch_reduce_partials((const double*)workspace, out_sum, s);
+    launch_reduce_partials(workspace, out_sum, nullptr, s);
     rc = check_hip("reduce_partials_kernel launch");
   }
   return rc;
@@ -478,7 +490,7 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   a.y_mean = y_mean;
   a.y_std = y_std;
   a.out = out;
-  a.partials = workspace ? workspace + 1 : nullptr;
+  a.partials = workspace ? workspace + 2 : nullptr;
   a.y_bstride = y_bstride;
   a.B = B;
   a.d = d;
@@ -502,7 +514,7 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   int32_t rc = check_hip("posterior_dense_kernel launch");
   if (rc != NFN_OK) return rc;
   if (out_sum) {
-    launch_reduce_partials((const double*)workspace, out_sum, s);
+    launch_reduce_partials(workspace, out_sum, nullptr, s);
     rc = check_hip("reduce_partials_kernel launch");
   }
   return rc;
@@ -711,19 +723,19 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   (void)d;
   (void)P;
   if (B <= 0) return 0;
-  return 1 + partials_capacity(B, P);  // [count | partials]
+  return partials_doubles(B, P);  // [count | non-finite | (sum, count) pairs]
 }
 
 int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   if (B <= 0) return 0;
-  // [count | partials | draw-split region: (max, sum) float2 per (range, sample)]
-  return 1 + partials_capacity(B, P) + (int64_t)posterior_split(B, tile_geom(P < 0 ? 0 : P).rows) * B;
+  // [count | non-finite | pairs | draw-split region: (max, sum) float2 per (range, sample)]
+  return partials_doubles(B, P) + (int64_t)posterior_split(B) * B;
 }
 
-int32_t nfn_reduce_partials_f64(const double* workspace, double* out, void* stream) {
+int32_t nfn_reduce_partials_f64(double* workspace, double* out_sum, double* out_nonfinite, void* stream) {
   g_last_error.clear();
-  if (!workspace || !out) return fail(NFN_E_NULLPTR, "workspace or out is NULL");
-  launch_reduce_partials(workspace, out, reinterpret_cast<hipStream_t>(stream));
+  if (!workspace || !out_sum) return fail(NFN_E_NULLPTR, "workspace or out_sum is NULL");
+  launch_reduce_partials(workspace, out_sum, out_nonfinite, reinterpret_cast<hipStream_t>(stream));
   return check_hip("reduce_partials_kernel launch");
 }
 

@@ -1,7 +1,7 @@
 // nfn_comm.hip — multi-GPU reduction of the mean log-likelihood over RCCL
 // (SURVEY.md §8(e)).  Samples are independent, so each rank evaluates its own
-// batch slice; the only exchange is one 16-byte all-reduce of {sum, count} in
-// fp64 — the distributed form of BaseEstimator.score's .mean()
+// batch slice; the only exchange is one 24-byte all-reduce of {sum, count,
+// non-finite count} in fp64 — the distributed form of BaseEstimator.score's .mean()
 // (estimators/BaseEstimator.py:43-47, evaluation/scorers.py:30-34).
 // Everything is stream-ordered on the caller's stream: no host synchronisation.
 #include <rccl/rccl.h>
@@ -20,9 +20,10 @@ int32_t comm_fail(ncclResult_t r, const char* what) {
 }
 
 __global__ void pack_sum_count_kernel(const double* __restrict__ local_sum, double count,
-                                      double* __restrict__ sum_count) {
+                                      const double* __restrict__ local_nf, double* __restrict__ sum_count) {
   sum_count[0] = local_sum[0];
   sum_count[1] = count;
+  sum_count[2] = local_nf ? local_nf[0] : 0.0;
 }
 
 __global__ void finish_mean_kernel(const double* __restrict__ sum_count, double* __restrict__ mean) {
@@ -64,16 +65,16 @@ int32_t nfn_comm_destroy(void* comm) {
   return r == ncclSuccess ? NFN_OK : comm_fail(r, "ncclCommDestroy");
 }
 
-int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, double* sum_count,
-                           double* mean_out, void* stream) {
+int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, const double* local_nonfinite,
+                           double* sum_count, double* mean_out, void* stream) {
   if (!comm || !local_sum || !sum_count)
     return set_error(NFN_E_NULLPTR, "nfn_allreduce_mean: NULL comm, local_sum or sum_count");
   if (local_count < 0) return set_error(NFN_E_SHAPE, "nfn_allreduce_mean: negative local_count");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  pack_sum_count_kernel<<<1, 1, 0, s>>>(local_sum, (double)local_count, sum_count);
+  pack_sum_count_kernel<<<1, 1, 0, s>>>(local_sum, (double)local_count, local_nonfinite, sum_count);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NFN_E_HIP, hipGetErrorString(e));
-  const ncclResult_t r = ncclAllReduce(sum_count, sum_count, 2, ncclFloat64, ncclSum,
+  const ncclResult_t r = ncclAllReduce(sum_count, sum_count, 3, ncclFloat64, ncclSum,
                                        static_cast<ncclComm_t>(comm), s);
   if (r != ncclSuccess) return comm_fail(r, "ncclAllReduce");
   if (mean_out) {

@@ -23,7 +23,7 @@ template <int DM, bool FAST, int NVH>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -72,6 +72,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
   };
 
   double acc_sum = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   int64_t tile = u0;
   if (tile < a.ntiles) issue(tile);
   for (; tile < a.ntiles; tile += ustep) {
@@ -130,15 +131,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
         lp = eval_chain<DM, FAST>(z, row, a) - corr;
       if (a.out) __builtin_nontemporal_store(lp, a.out + b0 + lane);
       acc_sum += (double)lp;
+      nfc += nonfinite1(lp);
     }
     wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
   }
   if (a.partials) {
-    const double sum = block_sum(acc_sum, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc_sum, nfc, red);
   }
 }
 
@@ -152,7 +150,7 @@ template <int QH, int NN>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   constexpr int H = 4 * QH;
   constexpr int RSTEP = 64 / QH;  // h rows per wave-instruction
   constexpr int kNT = 2;
@@ -216,6 +214,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
       buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, k * kstep, kNT));
   };
   double acc_sum = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
   float pend_v = 0.0f;
   auto flush = [&]() {
@@ -267,18 +266,17 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
     wave_lds_sync();
     const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS>(z0, tl + lane, a)
                                      : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
-    if (lane < nr) acc_sum += (double)lp;
+    if (lane < nr) {
+      acc_sum += (double)lp;
+      nfc += nonfinite1(lp);
+    }
     pend_v = lp;
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
     wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
   }
   flush();
   if (a.partials) {
-    const double sum = block_sum(acc_sum, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc_sum, nfc, red);
   }
 }
 
@@ -294,7 +292,7 @@ template <int QH, int NN>
 __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   constexpr int RSTEP = 64 / QH;
   constexpr int kNT = 2;
   const int tid = threadIdx.x;
@@ -355,6 +353,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
       bbuf[nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (16 * nt + am) * 4, 0, 0));
   };
   double acc_sum = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
   float pend_v = 0.0f;
   auto flush = [&]() {
@@ -416,17 +415,16 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
       wave_lds_sync();  // this unit's LDS reads done before the next unit's writes
     }
     const float res = lse_finish<true>(m, lacc, S);
-    if (lane < nr) acc_sum += (double)res;
+    if (lane < nr) {
+      acc_sum += (double)res;
+      nfc += nonfinite1(res);
+    }
     pend_v = res;
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
   }
   flush();
   if (a.partials) {
-    const double sum = block_sum(acc_sum, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc_sum, nfc, red);
   }
 }
 
@@ -438,7 +436,7 @@ template <int DM, bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) posterior_dense_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -459,6 +457,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense_kernel(DenseArgs da
     for (int j = 0; j < a.d; ++j) corr += f_log<FAST>(a.y_std[j]);
   }
   double acc_sum = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   for (int64_t tile = u0; tile < a.ntiles; tile += ustep) {
     const int64_t b0 = tile * 64;
     const int nr = (int)min((int64_t)64, a.B - b0);
@@ -516,14 +515,11 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense_kernel(DenseArgs da
       const float res = lse_finish<FAST>(m, lacc, a.S);
       if (a.out) __builtin_nontemporal_store(res, a.out + b0 + lane);
       acc_sum += (double)res;
+      nfc += nonfinite1(res);
     }
   }
   if (a.partials) {
-    const double sum = block_sum(acc_sum, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc_sum, nfc, red);
   }
 }
 

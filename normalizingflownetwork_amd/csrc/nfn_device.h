@@ -96,6 +96,7 @@ struct ChainArgs {
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
+  int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   FlowProgram prog;
 };
 
@@ -221,6 +222,22 @@ __device__ __forceinline__ float softplus_tf(float x) {
   }
 }
 
+// Radial alpha = softplus(0.3 a - 2) (RadialFlow.py:24-27) feeds h = 1 / (alpha + r),
+// so it needs RELATIVE accuracy as alpha -> 0: in the fast form ln(1 + e) rounds to 0
+// once e < 2^-24 (alpha = 0, h = inf at z == gamma, where TF stays finite).  Below
+// x = -5 (e < 6.7e-3) use log1p(e) = e (1 - e (1/2 - e/3)), relative error < 1e-7.
+template <bool FAST>
+__device__ __forceinline__ float softplus_alpha(float x) {
+  if constexpr (FAST) {
+    const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+    const float l = fmaf(__builtin_amdgcn_logf(1.0f + e), kLn2, fmaxf(x, 0.0f));
+    const float sr = e * fmaf(-e, fmaf(e, -1.0f / 3.0f, 0.5f), 1.0f);
+    return x < -5.0f ? sr : l;
+  } else {
+    return softplus_tf<false>(x);
+  }
+}
+
 template <bool FAST>
 __device__ __forceinline__ float f_tanh(float a) {
   if constexpr (FAST) {
@@ -294,7 +311,7 @@ __device__ __forceinline__ float planar_step(float (&z)[DM], PTR p, int d) {
 // _forward :54-56, _forward_log_det_jacobian :62-70 (der_h = RealDiv grad ((-1/y)/y)).
 template <int DM, bool FAST, typename PTR>
 __device__ __forceinline__ float radial_step(float (&z)[DM], PTR p, int d) {
-  const float alpha = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
+  const float alpha = softplus_alpha<FAST>(0.3f * p[0] - 2.0f);
   const float beta = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
   float r = 0.0f;
 #pragma unroll
@@ -430,7 +447,7 @@ __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, flo
 // alpha * beta = alpha * sp - alpha, and 1 + abh + ab * (-h^2) * r = 1 + abh * (alpha h)
 // because 1 - h r = alpha h.
 __device__ __forceinline__ float radial1_fast(float& z, float a0, float b0, float g) {
-  const float alpha = sp_fast1(fmaf(0.3f, a0, -2.0f));
+  const float alpha = softplus_alpha<true>(fmaf(0.3f, a0, -2.0f));
   const float ab = fmaf(alpha, sp_fast1(fmaf(0.1f, b0, kLogExpm1One)), -alpha);
   const float dz = z - g;
   const float h = __builtin_amdgcn_rcpf(alpha + fabsf(dz));
@@ -613,6 +630,41 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;
 }
 
+// 1 for a non-finite log_prob (inf / NaN), else 0: every kernel that writes partial
+// sums also counts these (SURVEY.md §5 — the reference only notices them in training,
+// TerminateOnNaN, BaseEstimator.py:29; score's .mean() silently returns -inf / NaN).
+__device__ __forceinline__ int nonfinite1(float v) { return __builtin_isfinite(v) ? 0 : 1; }
+
+// Workspace partials: pairs (sum, non-finite count) per workgroup at partials[2 blk],
+// partials[2 blk + 1]; the header partials[-2] (= workspace[0]) is the number of
+// pairs, partials[-1] (= workspace[1]) is filled by the reduction.  `red` holds
+// 2 * kMaxBlock / 64 doubles.  Contains a __syncthreads: call from every thread.
+__device__ __forceinline__ void write_partial(double* partials, double acc, int nf, double* red) {
+  double c = (double)nf;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    acc += __shfl_xor(acc, off);
+    c += __shfl_xor(c, off);
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * wid] = acc;
+    red[2 * wid + 1] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0, n = 0.0;
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) {
+      s += red[2 * w];
+      n += red[2 * w + 1];
+    }
+    partials[2 * blockIdx.x] = s;
+    partials[2 * blockIdx.x + 1] = n;
+    if (blockIdx.x == 0) partials[-2] = (double)gridDim.x;  // workspace header: number of pairs
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
@@ -620,7 +672,7 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 template <int DM, bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int rows = a.tile_rows > 0 ? a.tile_rows : blockDim.x;
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * rows;
@@ -639,20 +691,14 @@ __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
     lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
     if (a.out) a.out[b] = lp;
   }
-  if (a.partials) {
-    const double s = block_sum(tid < nr ? (double)lp : 0.0, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = s;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
-  }
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red);
 }
 
 // Posterior: the same tile walk once per draw, with an online logsumexp over draws.
 template <int DM, bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int rows = a.tile_rows > 0 ? a.tile_rows : blockDim.x;
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * rows;
@@ -682,13 +728,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
     res = lse_finish<FAST>(m, acc, a.S);
     if (a.out) a.out[b0 + tid] = res;
   }
-  if (a.partials) {
-    const double s = block_sum(tid < nr ? (double)res : 0.0, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = s;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
-  }
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red);
 }
 
 // Persistent, software-pipelined version of the two kernels above (the hot path).
@@ -712,7 +752,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <int DM, bool FAST, int NV, bool POST, bool PACKED>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArgs a) {
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int T = blockDim.x;
   const int tid = threadIdx.x;
   const int Q = a.P >> 2;
@@ -800,6 +840,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
   };
 
   double acc = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   // The store of a unit's results is deferred to the next unit and issued BEFORE
   // that unit's prefetch: vmcnt counts stores and loads in issue order, so a
   // store issued after the prefetch would make the next wait for the prefetched
@@ -884,6 +925,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
         pend_b = b0 + lt;
         pend_v = res;
         acc += (double)res;
+        nfc += nonfinite1(res);
       }
     }
   }
@@ -895,11 +937,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     }
   }
   if (a.partials && (!POST || nsp == 1)) {
-    const double sum = block_sum(acc, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc, nfc, red);
   }
 }
 
@@ -923,7 +961,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
 template <bool FAST, int Q, bool PACKED>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   constexpr int RSTEP = 64 / Q;  // rows per wave-instruction
   constexpr int kNT = 2;         // buffer cache policy: non-temporal (streamed once)
   const int tid = threadIdx.x;
@@ -969,6 +1007,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   };
 
   double acc = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   // The previous tile's log_prob, stored through a descriptor bounded at B (empty
   // before the first tile: the store is always issued).  It is issued right AFTER
   // the next prefetch, so the next hand-off's wait (vmcnt(1)) does not cover it.
@@ -1003,18 +1042,17 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       float z[1] = {z0};
       lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
     }
-    if (lane < nr) acc += (double)lp;
+    if (lane < nr) {
+      acc += (double)lp;
+      nfc += nonfinite1(lp);
+    }
     pend_v = lp;
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
     wave_lds_sync();  // this tile's LDS reads done before the next writes
   }
   flush();
   if (a.partials) {
-    const double sum = block_sum(acc, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc, nfc, red);
   }
 }
 
@@ -1024,7 +1062,7 @@ template <bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2* __restrict__ parts, int nsplit,
                                                                      int S, int64_t B, float* __restrict__ out,
                                                                      double* __restrict__ partials) {
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float res = 0.0f;
   if (b < B) {
@@ -1049,13 +1087,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2
     }
     if (out) out[b] = res;
   }
-  if (partials) {
-    const double sum = block_sum(b < B ? (double)res : 0.0, red);
-    if (threadIdx.x == 0) {
-      partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
-  }
+  if (partials) write_partial(partials, b < B ? (double)res : 0.0, b < B ? nonfinite1(res) : 0, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -1145,7 +1177,7 @@ __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int 
 template <int G, int DPL, bool FAST, bool FULL = false>
 __device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int d_, int j) {
   const int d = FULL ? G * DPL : d_;
-  const float alpha = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
+  const float alpha = softplus_alpha<FAST>(0.3f * p[0] - 2.0f);
   const float beta = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
   float g[DPL];
   float sr = 0.0f;
@@ -1248,7 +1280,7 @@ __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row
 template <int G, int DPL, bool FAST, int NV, bool POST>
 __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   const int T = blockDim.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1300,6 +1332,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     for (int i = 0; i < a.d; ++i) corr += f_log<FAST>(a.y_std[i]);
   }
   double acc = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   int64_t pend_b = -1;  // deferred store, see chain_persistent_kernel
   float pend_v = 0.0f;
   int64_t tile = u0;
@@ -1370,15 +1403,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
       pend_b = b0 + sl;
       pend_v = res;
       acc += (double)res;
+      nfc += nonfinite1(res);
     }
   }
   if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
   if (a.partials) {
-    const double sum = block_sum(acc, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc, nfc, red);
   }
 }
 
@@ -1392,7 +1422,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
 template <int G, int DPL, bool FAST, int NV, bool FULL>
 __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
-  __shared__ double red[kMaxBlock / 64];
+  __shared__ double red[2 * kMaxBlock / 64];
   constexpr int R = 64 / G;  // samples per wave tile
   constexpr int kNT = 2;
   const int tid = threadIdx.x;
@@ -1447,6 +1477,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   }
   const bool norm = a.y_mean != nullptr;
   double acc = 0.0;
+  int nfc = 0;  // non-finite log_prob values
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
   float pend_v = 0.0f;
   issue(u0);
@@ -1468,7 +1499,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     const float lp = eval_chain_gd<G, DPL, FAST, FULL>(z, tl + sl * S, a, j) - corr;
     wave_lds_sync();  // this tile's LDS reads done before the next writes
-    if (j == 0 && sl < nr) acc += (double)lp;
+    if (j == 0 && sl < nr) {
+      acc += (double)lp;
+      nfc += nonfinite1(lp);
+    }
     // lane i < R takes sample i's value (held by its group's lanes): one 64 B store
     // from 16 lanes instead of 4 identical copies per sample; lanes >= nr fall
     // outside the descriptor and are dropped
@@ -1477,11 +1511,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   }
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
   if (a.partials) {
-    const double sum = block_sum(acc, red);
-    if (tid == 0) {
-      a.partials[blockIdx.x] = sum;
-      if (blockIdx.x == 0) a.partials[-1] = (double)gridDim.x;  // workspace header: count
-    }
+    write_partial(a.partials, acc, nfc, red);
   }
 }
 

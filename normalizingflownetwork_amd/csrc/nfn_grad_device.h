@@ -105,7 +105,7 @@ template <int DM, bool FAST>
 __device__ __forceinline__ void radial_bwd(const float (&z)[DM], float (&a)[DM], float* p, int d, float gl) {
   const float xa = 0.3f * p[0] - 2.0f;
   const float xb = 0.1f * p[1] + kLogExpm1One;
-  const float al = softplus_tf<FAST>(xa);
+  const float al = softplus_alpha<FAST>(xa);
   const float be = softplus_tf<FAST>(xb) - 1.0f;
   float dz[DM];
   float r = 0.0f, da = 0.0f;
@@ -201,7 +201,7 @@ __device__ __forceinline__ void planar1_z(float& z, float u, float wraw, float b
 }
 
 __device__ __forceinline__ void radial1_z(float& z, float a0, float b0, float g) {
-  const float alpha = sp_fast1(fmaf(0.3f, a0, -2.0f));
+  const float alpha = softplus_alpha<true>(fmaf(0.3f, a0, -2.0f));
   const float ab = fmaf(alpha, sp_fast1(fmaf(0.1f, b0, kLogExpm1One)), -alpha);
   const float dz = z - g;
   z = fmaf(ab * __builtin_amdgcn_rcpf(alpha + fabsf(dz)), dz, z);
@@ -243,6 +243,7 @@ __device__ __forceinline__ void radial1_bwd(float z, float& a, float p0, float p
   const float xb = fmaf(0.1f, p1, kLogExpm1One);
   float al, sga, spb, sgb;
   sp_sig1(xa, al, sga);
+  al = xa < -5.0f ? softplus_alpha<true>(xa) : al;  // relative accuracy as alpha -> 0
   sp_sig1(xb, spb, sgb);
   const float be = spb - 1.0f;
   const float dz = z - p2;
@@ -444,6 +445,7 @@ __device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[
   float al, sga, spb, sgb;
   if constexpr (FAST) {
     sp_sig1(xa, al, sga);
+    al = xa < -5.0f ? softplus_alpha<true>(xa) : al;  // relative accuracy as alpha -> 0
     sp_sig1(xb, spb, sgb);
   } else {
     al = softplus_tf<false>(xa);

@@ -24,12 +24,13 @@ void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) 
     // math is short enough to hide); NFN_WG_PER_CU overrides
     int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);
     if (env_int("NFN_WG_PER_CU", 0) <= 0) grid = std::min<int64_t>(grid, (int64_t)cu_count() * 2);
+    grid = cap_grid(grid, a);
     *grid_out = grid;
     hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
     return;
   }
   auto kfn = chain_group_kernel<G, DPL, kFast, NV, POST>;
-  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4);  // 4 wave teams per WG
+  const int64_t grid = cap_grid(persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4), a);  // 4 wave teams per WG
   *grid_out = grid;
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
 }

@@ -16,10 +16,21 @@ namespace nfn {
 // Record `msg` as this thread's nfn_last_error() and return `code` (nfn_api.hip).
 int32_t set_error(int32_t code, const char* msg);
 
-// Tuning / diagnostic knobs (environment, read per launch).
+// Tuning / diagnostic knobs.  Only the NFN_DIAG build (libnfn_hip_diag.so, built for
+// tools/microbench.py) reads them from the environment; in the release library every
+// knob is its measured default, so no environment variable can change a result.
+#ifdef NFN_DIAG
 inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
+}
+#else
+inline int env_int(const char*, int dflt) { return dflt; }
+#endif
+
+// A persistent grid never exceeds the workspace's partial slots (ChainArgs::grid_cap).
+inline int64_t cap_grid(int64_t grid, const ChainArgs& a) {
+  return a.grid_cap > 0 ? std::min(grid, a.grid_cap) : grid;
 }
 
 inline int cu_count() {
@@ -78,7 +89,7 @@ void launch_sample(bool fast, int dm, const SampleArgs& sa, dim3 grid, dim3 bloc
 // nfn_grid.hip
 void launch_grid(bool fast, int dm, const GridArgs& ga, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_misc.hip
-void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
+void launch_reduce_partials(double* ws, double* out, double* out_nf, hipStream_t s);
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);
 void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,
                             hipStream_t s);

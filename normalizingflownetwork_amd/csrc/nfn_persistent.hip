@@ -27,6 +27,7 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
     grid = persistent_grid(kfn, T, lds, (units + teams - 1) / teams);
   else
     grid = std::min<int64_t>((units + teams - 1) / teams, (int64_t)cu_count() * (a.prog.K >= 4 ? 2 : 4));
+  grid = cap_grid(grid, a);
   *grid_out = grid;
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }
@@ -55,7 +56,7 @@ void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gri
   // units = tiles x draw ranges; in wave mode a workgroup runs T/64 units at a time
   const int64_t units = a.ntiles * (POST ? a.nsplit : 1);
   const int teams = a.ownrow == 2 ? T / 64 : 1;
-  const int64_t grid = persistent_grid(kfn, T, lds, (units + teams - 1) / teams);
+  const int64_t grid = cap_grid(persistent_grid(kfn, T, lds, (units + teams - 1) / teams), a);
   *grid_out = grid;
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }

@@ -79,7 +79,7 @@ __device__ __forceinline__ void planar_inv(float (&z)[DM], const float* p, int d
 
 template <int DM, bool FAST>
 __device__ __forceinline__ void radial_inv(float (&z)[DM], const float* p, int d) {
-  const float al = softplus_tf<FAST>(0.3f * p[0] - 2.0f);
+  const float al = softplus_alpha<FAST>(0.3f * p[0] - 2.0f);
   const float be = softplus_tf<FAST>(0.1f * p[1] + kLogExpm1One) - 1.0f;
   float ro = 0.0f;
 #pragma unroll

@@ -155,13 +155,14 @@ class FlowDistribution:
             return lp.reshape(())
         return lp
 
-    def log_prob_sum(self, y, y_mean=None, y_std=None) -> torch.Tensor:
-        """``sum_b log_prob(y_b)`` in fp64, reduced on the device (no (B,) output written)."""
+    def log_prob_sum(self, y, y_mean=None, y_std=None, want_nonfinite: bool = False):
+        """``sum_b log_prob(y_b)`` in fp64, reduced on the device (no (B,) output written);
+        with ``want_nonfinite`` also the number of non-finite log-densities (fp64 scalar)."""
         P = _shape(self._t)[-1]
         yy, tt, _ = _broadcast_rows(y, self._t, self._n_dims, P)
-        _, s = ops.chain_log_prob(yy, tt, self._flow_types, self._n_dims, self._trainable, y_mean, y_std,
-                                  want_values=False, want_sum=True)
-        return s[0]
+        _, s, nf = ops.chain_log_prob(yy, tt, self._flow_types, self._n_dims, self._trainable, y_mean, y_std,
+                                      want_values=False, want_nonfinite=True)
+        return (s[0], nf[0]) if want_nonfinite else s[0]
 
     def prob(self, y, y_mean=None, y_std=None):
         return torch.exp(self.log_prob(y, y_mean, y_std))

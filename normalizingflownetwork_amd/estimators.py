@@ -96,6 +96,7 @@ class BaseEstimator:
         # fit: the output Dense layer fused into the chain kernels (forward + backward)
         # when its shapes allow; False trains through the materialised t instead
         self.fused_dense = True
+        self.last_score_nonfinite = 0
         if n_dims_x is not None:
             self._build(n_dims_x)
 
@@ -183,12 +184,26 @@ class BaseEstimator:
         fused = self._fused_dense_inputs(x_data)
         if fused is not None:  # output Dense layer fused into the chain kernel
             dl = self.dist_layer
-            _, s = ops.chain_log_prob_dense(y_data, *fused, dl.flow_types, self.n_dims, dl.trainable_base_dist,
-                                            self.y_mean, self.y_std, want_values=False, want_sum=True)
-            return float(s.item()) / int(y_data.shape[0])
-        output = self(x_data)
-        s = output.log_prob_sum(y_data, self.y_mean, self.y_std)
-        return float(s.item()) / int(y_data.shape[0])
+            _, s, nf = ops.chain_log_prob_dense(y_data, *fused, dl.flow_types, self.n_dims, dl.trainable_base_dist,
+                                                self.y_mean, self.y_std, want_values=False, want_nonfinite=True)
+        else:
+            output = self(x_data)
+            s, nf = output.log_prob_sum(y_data, self.y_mean, self.y_std, want_nonfinite=True)
+        return self._finish_score(s, nf, int(y_data.shape[0]))
+
+    def _finish_score(self, s: torch.Tensor, nf: torch.Tensor, n: int) -> float:
+        """Mean from the device fp64 sum.  Non-finite log-densities propagate into the
+        mean exactly as in the reference's ``.mean()`` (``BaseEstimator.py:47``); their
+        count (kept as ``last_score_nonfinite``) is reported with a ``RuntimeWarning``
+        instead of passing silently."""
+        vals = torch.cat([s.reshape(1), nf.reshape(1)]).cpu().tolist()
+        self.last_score_nonfinite = int(vals[1])
+        if self.last_score_nonfinite:
+            import warnings
+
+            warnings.warn(f"score: {self.last_score_nonfinite} of {n} log-densities are not finite",
+                          RuntimeWarning, stacklevel=3)
+        return vals[0] / n
 
     def _assign_noise_regularisation(self, n_dims: int, n_datapoints: int):
         """``BaseEstimator.py:33-41``."""
@@ -296,29 +311,68 @@ class NormalizingFlowNetwork(BaseEstimator):
                                       learning_rate=learning_rate, activation=activation)
 
 
+def mean_field_scale(rho: torch.Tensor) -> torch.Tensor:
+    """Scale of the mean-field posterior over every DenseVariational weight:
+    ``1e-3 + softplus(log(expm1(1)) + 0.05 * rho)`` (``MeanFieldLayer``,
+    ``DistributionLayers.py:45-55``)."""
+    return 1e-3 + torch.nn.functional.softplus(float(np.log(np.expm1(1.0))) + 0.05 * rho)
+
+
 class BayesNormalizingFlowNetwork(BaseEstimator):
     """Posterior-scoring half of ``estimators/BayesNormalizingFlowNetwork.py`` /
-    ``BayesianNNEstimator.py``.  The weight posterior is mean-field Gaussian
-    (``BayesianNNEstimator.py:92-107``); each posterior draw re-samples the MLP
-    weights and yields a ``t`` draw.  ``score`` stacks the S draws as
-    ``t (S, B, P)`` and evaluates ``logsumexp_s(log_pdf) - log S`` per sample in
-    ONE fused kernel (``nfn_posterior_lse_f32``, or ``nfn_posterior_lse_dense_f32`` with the
-    output layer fused) instead of S model re-runs."""
+    ``BayesianNNEstimator.py``.  Every layer is a ``DenseVariational`` whose weights
+    (kernel and bias) have a mean-field Gaussian posterior held as one variable vector
+    ``[loc | rho]`` initialised N(0, 0.05) (Keras ``"normal"``; ``BayesianNNEstimator.py:92-107``,
+    ``DistributionLayers.py:17-55``): a draw is ``loc + (1e-3 + softplus(log(e-1) + 0.05 rho))
+    * eps``, one weight sample per layer per draw shared by the batch (``:122-145``); in
+    ``map_mode`` the variable holds ``loc`` only and the weights ARE ``loc``.  ``score``
+    stacks the S draws' last hidden activations and output-layer weights and evaluates
+    ``logsumexp_s(log_pdf) - log S`` per sample in ONE fused kernel
+    (``nfn_posterior_lse_dense_f32``, the output DenseVariational layer fused; or
+    ``nfn_posterior_lse_f32`` over a library-GEMM ``t``) instead of S model re-runs.
+    ``fit`` trains the posterior means by maximum likelihood; the KL(q || p) term and
+    the scales' training are not mirrored (out of scope)."""
 
     def __init__(self, n_dims, kl_weight_scale=1.0, n_flows=2, trainable_base_dist=True, flow_types=None,
                  hidden_sizes=(10,), activation="tanh", noise_reg=("fixed_rate", 0.0), learning_rate=2e-2,
-                 map_mode=False, prior_scale=1.0, posterior_scale=0.05, random_seed=22, n_dims_x=None):
+                 map_mode=False, prior_scale=1.0, trainable_prior=False, kl_use_exact=True, random_seed=22,
+                 n_dims_x=None):
         assert kl_weight_scale <= 1.0  # BayesianNNEstimator.py:120
         flow_types = tuple(flow_types) if flow_types is not None else ("radial",) * n_flows
         dist_layer = InverseNormalizingFlowLayer(flow_types=flow_types, n_dims=n_dims,
                                                  trainable_base_dist=trainable_base_dist)
         self.map_mode = map_mode
         self.prior_scale = prior_scale
-        self.posterior_scale = posterior_scale
+        self.trainable_prior = trainable_prior
+        self.kl_use_exact = kl_use_exact
         self.kl_weight_scale = kl_weight_scale
+        self.learning_rate = learning_rate  # BayesianNNEstimator.py:61-63 (Adam(learning_rate))
+        self._post_rho = None
         super().__init__(dist_layer, n_dims_x=n_dims_x, hidden_sizes=hidden_sizes, activation=activation,
                          random_seed=random_seed, noise_reg=noise_reg)
         self._draw_gen = None
+
+    def _build(self, n_dims_x: int):
+        """Shapes from the Dense stack; the posterior variables replace its weights: the
+        means ``loc`` live in ``self._mlp`` (so ``params`` is the posterior-mean network),
+        the ``rho`` in ``self._post_rho`` (None in map mode)."""
+        super()._build(n_dims_x)
+        g = torch.Generator().manual_seed(int(self.random_seed) + 1)
+        rhos = []
+        for w, b in zip(self._mlp.weights, self._mlp.biases):
+            size = w.numel() + b.numel()  # DenseVariational: kernel (in x units) then bias
+            v = 0.05 * torch.randn((size if self.map_mode else 2 * size,), generator=g, dtype=torch.float32)
+            w.copy_(v[:w.numel()].reshape(w.shape))
+            b.copy_(v[w.numel():size])
+            if not self.map_mode:
+                rhos.append((v[size:size + w.numel()].reshape(w.shape).clone(), v[size + w.numel():].clone()))
+        self._post_rho = None if self.map_mode else rhos
+
+    def posterior_scales(self, device=None):
+        """Per layer ``(scale_W, scale_b)`` of the mean-field posterior (None in map mode)."""
+        if self._post_rho is None:
+            return None
+        return [(mean_field_scale(rw).to(device), mean_field_scale(rb).to(device)) for rw, rb in self._post_rho]
 
     def _last_layer_draws(self, x, n_draws: int):
         """Per posterior draw: the last hidden activations and the sampled output layer,
@@ -337,16 +391,16 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
         xs = torch.as_tensor(self.x_std, dtype=torch.float32, device=dev)
         xn = (x - xm) / (xs + 1e-8)
         act = _ACTIVATIONS[self.activation]
+        scales = self.posterior_scales(dev)
         hs, ws, bs = [], [], []
+        n = len(self._mlp.weights)
         for _ in range(n_draws):
             h = xn
-            n = len(self._mlp.weights)
             for i, (w, b) in enumerate(zip(self._mlp.weights, self._mlp.biases)):
-                if not self.map_mode:
-                    w = w + self.posterior_scale * torch.randn(w.shape, generator=self._draw_gen, device=dev,
-                                                               dtype=torch.float32)
-                    b = b + self.posterior_scale * torch.randn(b.shape, generator=self._draw_gen, device=dev,
-                                                               dtype=torch.float32)
+                if scales is not None:  # a sample of q(w) = N(loc, scale^2), map mode: the mean
+                    sw, sb = scales[i]
+                    w = w + sw * torch.randn(w.shape, generator=self._draw_gen, device=dev, dtype=torch.float32)
+                    b = b + sb * torch.randn(b.shape, generator=self._draw_gen, device=dev, dtype=torch.float32)
                 if i < n - 1:
                     h = act(h @ w + b)
                 else:
@@ -366,7 +420,7 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
         never written to memory) when its width allows, else t is formed by the library GEMM."""
         S = n_draws if n_draws is not None else (1 if self.map_mode else 50)
         h, W, b = self._last_layer_draws(np.asarray(x_data, np.float32), S)
-        _, s = ops.posterior_lse_dense(np.asarray(y_data, np.float32), h, W, b, self.dist_layer.flow_types,
-                                       self.n_dims, self.dist_layer.trainable_base_dist, self.y_mean, self.y_std,
-                                       want_values=False, want_sum=True)
-        return float(s.item()) / int(np.shape(y_data)[0])
+        _, s, nf = ops.posterior_lse_dense(np.asarray(y_data, np.float32), h, W, b, self.dist_layer.flow_types,
+                                           self.n_dims, self.dist_layer.trainable_base_dist, self.y_mean,
+                                           self.y_std, want_values=False, want_sum=True, want_nonfinite=True)
+        return self._finish_score(s, nf, int(np.shape(y_data)[0]))

@@ -8,7 +8,7 @@ There is no CPU fallback — without a GPU these raise ``RuntimeError``.
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Sequence, Tuple
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -16,9 +16,6 @@ import torch
 from . import _lib
 
 FLOW_IDS = {"planar": 0, "radial": 1, "affine": 2}
-
-_workspaces: dict = {}
-
 
 def _device() -> torch.device:
     if not torch.cuda.is_available():
@@ -71,12 +68,20 @@ def total_param_size(flow_types: Sequence[str], n_dims: int, trainable_base: boo
 
 
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
-    key = (device.type, device.index)
-    ws = _workspaces.get(key)
-    if ws is None or ws.numel() < n_doubles:
-        ws = torch.empty(max(1, n_doubles), dtype=torch.float64, device=device)
-        _workspaces[key] = ws
-    return ws
+    """A fresh workspace per call from torch's stream-aware caching allocator (cheap):
+    calls in flight on different streams or threads never share partials or the
+    posterior's split region.  ``ws[1]`` receives the call's non-finite count."""
+    return torch.empty(max(2, n_doubles), dtype=torch.float64, device=device)
+
+
+def _with_nonfinite(out, osum, ws, want_nonfinite: bool):
+    """``(out, sum)`` or, with ``want_nonfinite``, ``(out, sum, nonfinite)`` where
+    ``nonfinite`` is a (1,) fp64 device tensor: the number of inf / NaN values among the
+    summed log-densities (counted by the kernel next to the partial sums; SURVEY.md §5,
+    the reference's ``TerminateOnNaN``, ``BaseEstimator.py:29``)."""
+    if not want_nonfinite:
+        return out, osum
+    return out, osum, ws[1:2]
 
 
 def _prep_2d(x, width: int, name: str, device) -> torch.Tensor:
@@ -98,10 +103,12 @@ def chain_log_prob(
     y_std=None,
     want_values: bool = True,
     want_sum: bool = False,
-) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    want_nonfinite: bool = False,
+):
     """Fused ``log_prob(y | t)`` over the whole flow chain (one kernel launch).
 
-    Returns ``(log_prob (B,) float32 | None, sum (1,) float64 | None)``.
+    Returns ``(log_prob (B,) float32 | None, sum (1,) float64 | None)``, plus the
+    non-finite count (1,) fp64 when ``want_nonfinite`` (implies ``want_sum``).
     With ``y_mean``/``y_std`` it is ``BaseEstimator.log_pdf``'s
     ``log_prob((y-mu)/sigma) - sum(log sigma)`` (``BaseEstimator.py:77-86``).
     """
@@ -116,6 +123,7 @@ def chain_log_prob(
         ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
         assert ym.numel() == n_dims and ys.numel() == n_dims
+    want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
     osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
@@ -127,7 +135,7 @@ def chain_log_prob(
         _ptr(out), _ptr(osum), _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_chain_logprob_f32")
-    return out, osum
+    return _with_nonfinite(out, osum, ws, want_nonfinite)
 
 
 def chain_log_prob_grad(
@@ -272,6 +280,7 @@ def chain_log_prob_dense(
     y_std=None,
     want_values: bool = True,
     want_sum: bool = False,
+    want_nonfinite: bool = False,
 ):
     """``log_prob(y | t = h W + b)`` with the estimator's output Dense layer
     (``MaximumLikelihoodNNEstimator.py:37-44``) fused into the chain kernel: ``h`` (B, H) last
@@ -287,7 +296,8 @@ def chain_log_prob_dense(
     bb = None if b is None else as_device_f32(b, dev).reshape(-1).contiguous()
     if not dense_fusable(H, P, n_dims) or h.stride(0) % 4 or h.data_ptr() % 16:
         t = h @ W + (bb if bb is not None else 0.0)
-        return chain_log_prob(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, want_values, want_sum)
+        return chain_log_prob(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, want_values, want_sum,
+                              want_nonfinite)
     y = _prep_2d(y, n_dims, "y", dev)
     B = int(h.shape[0])
     assert y.shape[0] in (1, B), "incompatible batch sizes"
@@ -295,6 +305,7 @@ def chain_log_prob_dense(
     if y_mean is not None:
         ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
     osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
@@ -306,7 +317,7 @@ def chain_log_prob_dense(
         _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_chain_logprob_dense_f32")
-    return out, osum
+    return _with_nonfinite(out, osum, ws, want_nonfinite)
 
 
 def chain_log_prob_dense_grad(
@@ -385,6 +396,7 @@ def posterior_lse_dense(
     y_std=None,
     want_values: bool = True,
     want_sum: bool = False,
+    want_nonfinite: bool = False,
 ):
     """Bayesian posterior score per sample with the output DenseVariational layer fused
     (``BayesianNNEstimator.py:65-76`` score over draws, ``:136-145`` the variational output
@@ -413,13 +425,15 @@ def posterior_lse_dense(
     if not dense_fusable(H, P, n_dims) or not aligned:
         hd = h if h.dim() == 3 else h.unsqueeze(0).expand(S, B, H)
         t = torch.matmul(hd, W) + (bb.unsqueeze(1) if bb is not None else 0.0)
-        return posterior_lse(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, want_values, want_sum)
+        return posterior_lse(y, t, flow_types, n_dims, trainable_base, y_mean, y_std, want_values, want_sum,
+                             want_nonfinite)
     y = _prep_2d(y, n_dims, "y", dev)
     assert y.shape[0] in (1, B), "incompatible batch sizes"
     ym = ys = None
     if y_mean is not None:
         ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
     osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
@@ -431,7 +445,7 @@ def posterior_lse_dense(
         _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_posterior_lse_dense_f32")
-    return out, osum
+    return _with_nonfinite(out, osum, ws, want_nonfinite)
 
 
 class DenseLauncher:
@@ -448,7 +462,7 @@ class DenseLauncher:
         self.y, self.h, self.W, self.b = y, h, W.contiguous(), b
         self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
         self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
-        self.partials = torch.empty((max(1, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
+        self.partials = torch.empty((max(2, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
                                     dtype=torch.float64, device=dev)
         self._ids, self._k = flow_ids(flow_types)
         self._args = (
@@ -463,11 +477,16 @@ class DenseLauncher:
             _lib.check(rc, "nfn_chain_logprob_dense_f32")
 
     def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
-        rc = self.lib.nfn_reduce_partials_f64(_ptr(self.partials), _ptr(self.sum),
+        rc = self.lib.nfn_reduce_partials_f64(_ptr(self.partials), _ptr(self.sum), None,
                                               stream if stream is not None else _stream())
         if rc != 0:
             _lib.check(rc, "nfn_reduce_partials_f64")
         return self.sum
+
+    @property
+    def nonfinite(self) -> torch.Tensor:
+        """(1,) fp64: non-finite values among the last reduced launch's log-densities."""
+        return self.partials[1:2]
 
 
 class PosteriorDenseLauncher(DenseLauncher):
@@ -487,7 +506,7 @@ class PosteriorDenseLauncher(DenseLauncher):
         self.b = None if b is None else b.contiguous()
         self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
         self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
-        self.partials = torch.empty((max(1, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
+        self.partials = torch.empty((max(2, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
                                     dtype=torch.float64, device=dev)
         self._ids, self._k = flow_ids(flow_types)
         self._args = (
@@ -596,6 +615,7 @@ def posterior_lse(
     y_std=None,
     want_values: bool = True,
     want_sum: bool = False,
+    want_nonfinite: bool = False,
 ):
     """``logsumexp_s(log_pdf(y_b | t[s, b])) - log S`` per sample (``BayesianNNEstimator.py:65-76``).
 
@@ -612,6 +632,7 @@ def posterior_lse(
     if y_mean is not None:
         ym = as_device_f32(y_mean, dev).reshape(-1).contiguous()
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
+    want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
     osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
@@ -624,7 +645,7 @@ def posterior_lse(
         _ptr(out), _ptr(osum), _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_posterior_lse_f32")
-    return out, osum
+    return _with_nonfinite(out, osum, ws, want_nonfinite)
 
 
 def set_math_mode(mode: str) -> str:
@@ -663,7 +684,7 @@ class ChainLauncher:
         self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
         fn_ws = self.lib.nfn_posterior_workspace_doubles if self.posterior else self.lib.nfn_chain_workspace_doubles
         self.n_partials = int(fn_ws(self.B, self.n_dims, self.P))
-        self.partials = torch.empty((max(1, self.n_partials),), dtype=torch.float64, device=dev)
+        self.partials = torch.empty((max(2, self.n_partials),), dtype=torch.float64, device=dev)
         self._ids, self._k = flow_ids(flow_types)
         self._ids_p = ctypes.cast(self._ids, ctypes.c_void_p)
         self._trainable = int(bool(trainable_base))
@@ -680,7 +701,7 @@ class ChainLauncher:
                 self._trainable, None, None, _ptr(self.out), None, _ptr(self.partials),
             )
             self._fn = self.lib.nfn_chain_logprob_f32
-        self._sum_args = (_ptr(self.partials), _ptr(self.sum))
+        self._sum_args = (_ptr(self.partials), _ptr(self.sum), None)
 
     def launch(self, stream: Optional[int] = None) -> None:
         rc = self._fn(*self._args, stream if stream is not None else _stream())
@@ -692,6 +713,11 @@ class ChainLauncher:
         if rc != 0:
             _lib.check(rc, "nfn_reduce_partials_f64")
         return self.sum
+
+    @property
+    def nonfinite(self) -> torch.Tensor:
+        """(1,) fp64: non-finite values among the last reduced launch's log-densities."""
+        return self.partials[1:2]
 
 
 class GradLauncher:
@@ -724,3 +750,40 @@ class GradLauncher:
         rc = self.lib.nfn_chain_logprob_grad_f32(*self._args, stream if stream is not None else _stream())
         if rc != 0:
             _lib.check(rc, "nfn_chain_logprob_grad_f32")
+
+
+class DenseGradLauncher:
+    """Pre-bound fused backward through the output Dense layer
+    (``nfn_chain_logprob_dense_grad_f32``) over fixed device buffers (the training-step
+    benchmark): ``launch()`` writes ``grad_h`` (B, H), ``grad_W`` (H, P), ``grad_b`` (P,)
+    and ``grad_y`` (B, d) for the upstream gradient ``g_out`` — one C-ABI call (the
+    fused kernel + the fixed-order partials sum)."""
+
+    def __init__(self, y: torch.Tensor, h: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor],
+                 flow_types: Sequence[str], n_dims: int, trainable_base: bool, g_out: Optional[torch.Tensor] = None):
+        self.lib = _lib.load()
+        dev = y.device
+        self.n_dims = int(n_dims)
+        self.P = total_param_size(flow_types, n_dims, trainable_base)
+        self.B, self.H = int(h.shape[0]), int(h.shape[1])
+        assert dense_fusable(self.H, self.P, self.n_dims) and h.stride(1) == 1 and h.stride(0) % 4 == 0
+        assert tuple(W.shape) == (self.H, self.P) and y.dim() == 2 and y.shape[1] == n_dims
+        assert g_out is None or (g_out.numel() == self.B and g_out.is_contiguous())
+        self.y, self.h, self.W, self.b, self.g_out = y, h, W.contiguous(), b, g_out
+        self.grad_h = torch.empty((self.B, self.H), dtype=torch.float32, device=dev)
+        self.grad_W = torch.empty((self.H, self.P), dtype=torch.float32, device=dev)
+        self.grad_b = torch.empty((self.P,), dtype=torch.float32, device=dev)
+        self.grad_y = torch.empty((self.B, self.n_dims), dtype=torch.float32, device=dev)
+        self.ws = torch.empty((max(1, int(self.lib.nfn_dense_grad_workspace_floats(self.B, self.H, self.P))),),
+                              dtype=torch.float32, device=dev)
+        self._ids, self._k = flow_ids(flow_types)
+        self._args = (
+            _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), self.H, _ptr(self.W), _ptr(b), self.B, self.n_dims,
+            ctypes.cast(self._ids, ctypes.c_void_p), self._k, int(bool(trainable_base)), None, None, _ptr(g_out),
+            None, _ptr(self.grad_h), self.H, _ptr(self.grad_W), _ptr(self.grad_b), _ptr(self.grad_y), _ptr(self.ws),
+        )
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self.lib.nfn_chain_logprob_dense_grad_f32(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_chain_logprob_dense_grad_f32")

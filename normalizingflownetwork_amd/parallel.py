@@ -3,7 +3,7 @@
 Samples are independent (``DistributionLayers.py:245-255`` has no cross-sample
 op), so every rank owns a contiguous slice of the batch, evaluates it with the
 fused kernel, and the ONLY collective is one all-reduce of ``(sum log_prob,
-count)`` in fp64 (16 bytes) — the distributed form of ``score``'s ``.mean()``
+count, non-finite count)`` in fp64 (24 bytes) — the distributed form of ``score``'s ``.mean()``
 (``BaseEstimator.py:47``, ``scorers.py:34``).  On MI355X the process group is
 ``nccl`` (= RCCL over xGMI); ``gloo`` works for CPU-side tests.
 
@@ -32,15 +32,18 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < rem else 0)
 
 
-def allreduce_sum_count(local_sum: torch.Tensor, local_count: int, group=None) -> torch.Tensor:
-    """All-reduce ``[sum, count]`` (fp64) across the group; returns the reduced pair.
-
-    The buffer lives where the backend needs it (device for nccl/RCCL, host for gloo)."""
+def allreduce_sum_count(local_sum: torch.Tensor, local_count: int, group=None,
+                        local_nonfinite: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """All-reduce ``[sum, count, non-finite count]`` (fp64) across the group; returns the
+    reduced triple.  The buffer lives where the backend needs it (device for nccl/RCCL,
+    host for gloo)."""
     backend = dist.get_backend(group) if dist.is_initialized() else None
     dev = local_sum.device if backend == "nccl" else torch.device("cpu")
-    buf = torch.empty((2,), dtype=torch.float64, device=dev)
+    buf = torch.zeros((3,), dtype=torch.float64, device=dev)
     buf[0] = local_sum.reshape(()).to(device=dev, dtype=torch.float64)
     buf[1] = float(local_count)
+    if local_nonfinite is not None:
+        buf[2] = local_nonfinite.reshape(()).to(device=dev, dtype=torch.float64)
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return buf
@@ -50,14 +53,24 @@ def mean_log_prob(
     y_shard, t_shard, flow_types: Sequence[str], n_dims: int, trainable_base: bool,
     y_mean=None, y_std=None, group=None,
 ) -> torch.Tensor:
-    """Mean of ``log_prob`` over the union of all ranks' shards (fp64, on every rank)."""
-    _, s = ops.chain_log_prob(y_shard, t_shard, flow_types, n_dims, trainable_base, y_mean, y_std,
-                              want_values=False, want_sum=True)
+    """Mean of ``log_prob`` over the union of all ranks' shards (fp64, on every rank).
+    Non-finite log-densities propagate into the mean as in the reference's ``.mean()``;
+    :func:`mean_log_prob_nonfinite` also returns their global count."""
+    return mean_log_prob_nonfinite(y_shard, t_shard, flow_types, n_dims, trainable_base, y_mean, y_std, group)[0]
+
+
+def mean_log_prob_nonfinite(
+    y_shard, t_shard, flow_types: Sequence[str], n_dims: int, trainable_base: bool,
+    y_mean=None, y_std=None, group=None,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``(mean log_prob, global non-finite count)`` over the union of all ranks' shards."""
+    _, s, nf = ops.chain_log_prob(y_shard, t_shard, flow_types, n_dims, trainable_base, y_mean, y_std,
+                                  want_values=False, want_sum=True, want_nonfinite=True)
     count = max(int(ops.as_device_f32(y_shard).reshape(-1, n_dims).shape[0]),
                 int(ops.as_device_f32(t_shard).shape[0]) if ops.total_param_size(flow_types, n_dims,
                                                                                   trainable_base) else 0)
-    buf = allreduce_sum_count(s, count, group)
-    return buf[0] / buf[1]
+    buf = allreduce_sum_count(s, count, group, local_nonfinite=nf)
+    return buf[0] / buf[1], buf[2]
 
 
 class NativeComm:
@@ -85,18 +98,23 @@ class NativeComm:
                                            self.rank), "nfn_comm_init")
         self.handle = handle
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.sum_count = torch.zeros((2,), dtype=torch.float64, device=dev)
+        self.sum_count = torch.zeros((3,), dtype=torch.float64, device=dev)  # sum, count, non-finite
         self.mean = torch.zeros((1,), dtype=torch.float64, device=dev)
 
-    def allreduce_mean(self, local_sum: torch.Tensor, local_count: int, stream=None) -> torch.Tensor:
-        """``{sum, count}`` summed over ranks into ``self.sum_count``; returns the
-        device scalar ``sum / count`` (``self.mean``).  Stream-ordered."""
+    def allreduce_mean(self, local_sum: torch.Tensor, local_count: int, stream=None,
+                       local_nonfinite: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``{sum, count, non-finite}`` summed over ranks into ``self.sum_count``; returns
+        the device scalar ``sum / count`` (``self.mean``).  Stream-ordered."""
         from . import _lib
 
         assert local_sum.dtype == torch.float64 and local_sum.is_cuda
         if stream is None:
             stream = torch.cuda.current_stream().cuda_stream
-        _lib.check(self._lib.nfn_allreduce_mean(self.handle, local_sum.data_ptr(), int(local_count),
+        nf_ptr = None
+        if local_nonfinite is not None:
+            assert local_nonfinite.dtype == torch.float64 and local_nonfinite.is_cuda
+            nf_ptr = local_nonfinite.data_ptr()
+        _lib.check(self._lib.nfn_allreduce_mean(self.handle, local_sum.data_ptr(), int(local_count), nf_ptr,
                                                 self.sum_count.data_ptr(), self.mean.data_ptr(), int(stream)),
                    "nfn_allreduce_mean")
         return self.mean

@@ -43,6 +43,49 @@ CHAIN_FIXTURES = [
 ]
 FLOW_FIXTURES = [f"flow_{f}_d{d}" for f in ("planar", "radial", "affine") for d in (1, 4)]
 
+# Parity margins measured by the GPU tests (written at session end when non-empty).
+PARITY = []
+# A sample admitted only through the fp32-conditioning term of oracle.tolerance_bound
+# (|gpu - ref64| > 1e-5 max(1, |ref64|)) must still be within WIDEN_CAP x |ref32 - ref64|.
+WIDEN_CAP = 2.0
+
+
+def record_parity(what, got, ref64, ref32, err, bound):
+    """Per check: the max of |gpu - ref64| / max(1, |ref64|); the max of |gpu - ref64| / |ref64|
+    over |ref64| < 1; the samples admitted only through the fp32-conditioning widening, their
+    count and max |gpu - ref64| / |ref32 - ref64|; the worst sample relative to its bound."""
+    ref64 = np.asarray(ref64, np.float64)
+    dev32 = np.abs(np.asarray(ref32, np.float64) - ref64)
+    base = 1e-5 * np.maximum(1.0, np.abs(ref64))
+    fin = np.isfinite(ref64) & np.isfinite(got)
+    small = fin & (np.abs(ref64) < 1.0) & (ref64 != 0.0)
+    widened = fin & (err > base)
+    w = int(np.argmax(np.where(fin, err / np.maximum(bound, 1e-300), -1.0)))
+    PARITY.append({
+        "check": what,
+        "n": int(ref64.size),
+        "nonfinite_ref": int((~np.isfinite(ref64)).sum()),
+        "max_err_over_max1ref": float((err[fin] / np.maximum(1.0, np.abs(ref64[fin]))).max()) if fin.any() else None,
+        "max_rel_err_small_ref": float((err[small] / np.abs(ref64[small])).max()) if small.any() else None,
+        "n_widened": int(widened.sum()),
+        "widened_max_err_over_dev32": float((err[widened] / np.maximum(dev32[widened], 1e-300)).max())
+        if widened.any() else None,
+        "widened_max_err_over_base": float((err[widened] / base[widened]).max()) if widened.any() else None,
+        "worst": {"idx": w, "got": float(np.ravel(got)[w]), "ref64": float(ref64.ravel()[w]),
+                  "ref32": float(np.ravel(ref32)[w]), "err_over_bound": float(np.ravel(err)[w] / np.ravel(bound)[w])},
+    })
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not PARITY:
+        return
+    import json
+
+    out = os.path.join(REPO, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "parity.json"), "w") as f:
+        json.dump({"widen_cap": WIDEN_CAP, "checks": PARITY}, f, indent=1)
+
 
 @pytest.fixture(scope="session")
 def native_lib():

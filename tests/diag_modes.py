@@ -1,0 +1,89 @@
+"""Subprocess body of tests/test_gpu_diag.py (one process, one GPU context).
+
+  python tests/diag_modes.py strategies   -- NFN_DIAG build: every tile-streaming strategy
+      (NFN_LOAD_MODE) gives bitwise-identical per-sample log_prob, and the draw-split
+      posterior agrees with the single-range one (NFN_POST_SPLIT=1)
+  python tests/diag_modes.py release      -- release build under ablation / tuning knobs in
+      the environment: results are the oracle's (the knobs are compiled out)
+Prints one JSON line; exits non-zero on a mismatch."""
+
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+from conftest import load_golden  # noqa: E402
+from oracle import nfn_oracle as O  # noqa: E402  (checker)
+
+
+def strategies():
+    import torch
+
+    from normalizingflownetwork_amd import _lib
+
+    _lib.use_diagnostic_build()
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden("stress_pr5_d1")
+    gp = load_golden("posterior_s8_pr5_d1")
+    ref, _ = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], 1, True)
+    pref, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
+    res = {}
+    for mode in ("coop", "wave", "ownrow", "tile"):
+        os.environ["NFN_LOAD_MODE"] = mode
+        try:
+            got, s = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], 1, True, want_sum=True)
+            pgot, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
+        finally:
+            os.environ.pop("NFN_LOAD_MODE")
+        assert torch.equal(got, ref), mode
+        assert abs(float(s.item()) - float(got.double().sum().item())) <= 1e-12 * abs(float(s.item())), mode
+        np.testing.assert_allclose(pgot.cpu().numpy(), pref.cpu().numpy(), rtol=2e-6, atol=2e-6)
+        res[mode] = "bitwise"
+    # C5 shape: draw split (default) vs one range
+    ft = ("planar", "radial") * 5
+    S, B = 64, 1 << 17
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    y = torch.randn((B, 1), generator=gen, device="cuda")
+    t = torch.randn((S, B, 32), generator=gen, device="cuda")
+    out, _ = ops.posterior_lse(y, t, ft, 1, True)
+    os.environ["NFN_POST_SPLIT"] = "1"
+    try:
+        out1, _ = ops.posterior_lse(y, t, ft, 1, True)
+    finally:
+        os.environ.pop("NFN_POST_SPLIT")
+    np.testing.assert_allclose(out.cpu().numpy(), out1.cpu().numpy(), rtol=2e-6, atol=2e-6)
+    res["post_split_vs_single"] = "allclose 2e-6"
+    res["library"] = os.path.basename(_lib.LIB_PATH)
+    return res
+
+
+def release():
+    from normalizingflownetwork_amd import _lib, ops
+
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("NFN_")}
+    assert knobs.get("NFN_ABLATE_FLOWS") == "1", "run with the knobs set"
+    res = {"library": os.path.basename(_lib.LIB_PATH), "knobs": knobs}
+    for name in ("c2_pr5_d1", "c3_apr_d8", "stress_pr5_d1"):
+        g = load_golden(name)
+        lp, _ = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], g["d"], bool(g["trainable"]))
+        err = np.abs(lp.cpu().numpy().astype(np.float64) - g["ref64"])
+        ok = err <= O.tolerance_bound(g["ref64"], g["ref32"])
+        assert ok.all(), f"{name}: {int((~ok).sum())} samples off under the knobs"
+        res[name] = "oracle parity"
+    gp = load_golden("posterior_s8_pr5_d1")
+    out, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
+    ok = np.abs(out.cpu().numpy() - gp["ref64"]) <= O.tolerance_bound(gp["ref64"], gp["ref32"])
+    assert ok.all()
+    res["posterior"] = "oracle parity"
+    return res
+
+
+if __name__ == "__main__":
+    which = sys.argv[1]
+    print(json.dumps({which: {"strategies": strategies, "release": release}[which]()}), flush=True)

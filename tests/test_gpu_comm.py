@@ -20,7 +20,7 @@ def test_native_comm_single_rank_mean(gpu):
         s = torch.tensor([12.5], dtype=torch.float64, device=gpu)
         m = comm.allreduce_mean(s, 5)
         torch.cuda.synchronize()
-        assert comm.sum_count.tolist() == [12.5, 5.0]
+        assert comm.sum_count.tolist() == [12.5, 5.0, 0.0]
         assert m.item() == 2.5
     finally:
         comm.close()

@@ -52,3 +52,36 @@ def test_bench_nccl_step_path_one_rank(gpu, allreduce):
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["n_gpus"] == 1 and np.isfinite(out["mean_log_prob"])
+
+
+def test_bench_spawns_its_ranks(gpu):
+    """`python bench.py --gpus 2` (no launcher): bench.py starts torch.distributed.run as a
+    child and the JSON line proves the process group's size (VERDICT r1 "Next" 1)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--backend", "gloo", "--batch", str(1 << 18), "--prewarm-ms", "20"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["pg_world_size"] == 2 and out["rank_devices"] == [0, 0]
+    assert out["config"]["global_batch"] == 2 * (1 << 18)
+    assert out["cpu_baseline"] is None  # rank 0 at N = 1 only
+    assert np.isfinite(out["mean_log_prob"]) and out["nonfinite_log_prob"] == 0
+
+
+def test_two_rank_reduction_matches_one_rank(gpu):
+    """The all-reduced mean over two ranks' shards equals one launch over the concatenated
+    batch (fp64, rel 1e-12), and the non-finite counts add up across ranks."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "tests", "mp_reduce.py")]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = {d["rank"]: d for d in (json.loads(l) for l in r.stdout.splitlines() if l.startswith("{"))}
+    assert sorted(res) == [0, 1] and res[0]["world"] == 2
+    assert res[0]["mean"] == res[1]["mean"]
+    assert res[0]["mean"] == pytest.approx(res[0]["one_rank_mean"], rel=1e-12)
+    assert res[0]["nonfinite"] == 0 and res[0]["nonfinite_poisoned"] == res[1]["nonfinite_poisoned"] == 3

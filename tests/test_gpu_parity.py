@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import CHAIN_FIXTURES, FLOW_FIXTURES, load_golden
+from conftest import CHAIN_FIXTURES, FLOW_FIXTURES, WIDEN_CAP, load_golden, record_parity
 from oracle import nfn_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -32,6 +32,8 @@ def math_mode(request, gpu):
 
 
 def assert_within(got, ref64, ref32, what, extra_rel=0.0):
+    """Per-sample parity check against the oracle tolerance; records the measured margins
+    (conftest.PARITY -> gpurun_out/parity.json, committed as profiles/r02_parity.json)."""
     got = np.asarray(got, np.float64)
     assert got.shape == np.shape(ref64), f"{what}: shape {got.shape} != {np.shape(ref64)}"
     if got.size == 0:
@@ -40,11 +42,21 @@ def assert_within(got, ref64, ref32, what, extra_rel=0.0):
     if extra_rel:
         bound = bound + extra_rel * np.maximum(1.0, np.abs(ref64))
     err = np.abs(got - ref64)
+    record_parity(what, got, ref64, ref32, err, bound)
     bad = ~(err <= bound)
     assert not bad.any(), (
         f"{what}: {bad.sum()} / {bad.size} samples outside tolerance; worst idx {int(np.argmax(err - bound))} "
         f"got {got[np.argmax(err - bound)]!r} ref {ref64[np.argmax(err - bound)]!r}"
     )
+    # samples admitted only through the fp32-conditioning term must stay within
+    # WIDEN_CAP x the reference's own fp32 deviation (measured: profiles/r02_parity.json)
+    base = O.REL_TOL * np.maximum(1.0, np.abs(ref64))
+    dev32 = np.abs(np.asarray(ref32, np.float64) - ref64)
+    widened = err > base
+    if widened.any():
+        assert (err[widened] <= WIDEN_CAP * dev32[widened]).all(), (
+            f"{what}: widened samples exceed {WIDEN_CAP} x |ref32 - ref64|: "
+            f"max ratio {float((err[widened] / dev32[widened]).max()):.3g}")
     return float((err / np.maximum(1.0, np.abs(ref64))).max())
 
 
@@ -304,43 +316,12 @@ def test_full_size_posterior_properties(gpu):
     ref64 = O.posterior_lse(yn, tn, ft, 1, True)
     ref32 = O.posterior_lse(yn, tn, ft, 1, True, dtype=np.float32)
     assert_within(out[idx].cpu().numpy(), ref64, ref32, "C5 sample")
-    # the draw-split path (default at this B) agrees with the single-range path
-    import os
-
-    os.environ["NFN_POST_SPLIT"] = "1"
-    try:
-        out1, _ = ops.posterior_lse(y, t, ft, 1, True)
-    finally:
-        os.environ.pop("NFN_POST_SPLIT")
-    np.testing.assert_allclose(out.cpu().numpy(), out1.cpu().numpy(), rtol=2e-6, atol=2e-6)
+    # (the draw-split path vs the single-range path: tests/test_gpu_diag.py, NFN_DIAG build)
     # S copies of one draw: lse - log S == log_prob
     rep = t[:1].expand(S, B, 32).contiguous()
     out_rep, _ = ops.posterior_lse(y, rep, ft, 1, True)
     lp, _ = ops.chain_log_prob(y, t[0], ft, 1, True)
     np.testing.assert_allclose(out_rep.cpu().numpy(), lp.cpu().numpy(), rtol=1e-5, atol=2e-5)
-
-
-@pytest.mark.parametrize("mode", ["coop", "wave", "ownrow", "tile"])
-def test_load_modes_bitwise_equal(mode, gpu):
-    """Every tile-streaming strategy evaluates each sample with the same math, so
-    the per-sample outputs are bitwise identical across strategies."""
-    import os
-
-    from normalizingflownetwork_amd import ops
-
-    g = load_golden("stress_pr5_d1")
-    ref, _ = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], 1, True)
-    gp = load_golden("posterior_s8_pr5_d1")
-    pref, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
-    os.environ["NFN_LOAD_MODE"] = mode
-    try:
-        got, s = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], 1, True, want_sum=True)
-        pgot, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])
-    finally:
-        os.environ.pop("NFN_LOAD_MODE")
-    assert torch.equal(got, ref)
-    assert float(s.item()) == pytest.approx(float(got.double().sum().item()), rel=1e-12)
-    np.testing.assert_allclose(pgot.cpu().numpy(), pref.cpu().numpy(), rtol=2e-6, atol=2e-6)
 
 
 @pytest.mark.parametrize("d,K", [(32, 64), (1, 64), (16, 40), (5, 64)])

@@ -1,0 +1,217 @@
+"""Workspace, reduction and multi-stream correctness of the C ABI (round-2 review items).
+
+* No launch writes past the workspace the library asks for: the posterior's draw-split
+  region (sized and bounded by ONE split function) and the per-workgroup partials of the
+  lane-group kernels (grids capped at the workspace's slots) — checked with a canary
+  after the region, through the C ABI.
+* The non-finite count the partials kernels keep next to the fp64 sum
+  equals the number of inf / NaN log-densities, on every kernel family.
+* Two streams in flight with their own workspaces give the single-stream results bitwise.
+* C4's per-GPU form at the full 8-GPU global batch: B = 2^27 on ONE device (t = 16 GiB,
+  offsets past 2^31 elements), against the oracle on samples spread over the batch.
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import nfn_oracle as O
+
+pytestmark = pytest.mark.gpu
+C2 = ("planar", "radial") * 5
+SENTINEL = 12345.678
+
+
+def _ids(ft):
+    from normalizingflownetwork_amd import ops
+
+    return ops.flow_ids(ft)
+
+
+def _canary_ws(n):
+    ws = torch.full((n + 64,), SENTINEL, dtype=torch.float64, device="cuda")
+    return ws
+
+
+def _check_canary(ws, n, what):
+    tail = ws[n:].cpu().numpy()
+    assert (tail == SENTINEL).all(), f"{what}: workspace overrun ({int((tail != SENTINEL).sum())} doubles past the end)"
+
+
+@pytest.mark.parametrize("S,B", [(16, 34817), (32, 34817), (16, 40000), (50, 34817), (3, 1000)])
+def test_posterior_split_stays_in_workspace(S, B, gpu):
+    """the split region was sized with 256-row tiles but launched with
+    64-row ones; B = 34817 with S = 16 or 32 overran it by one range."""
+    from normalizingflownetwork_amd import _lib
+
+    lib = _lib.load()
+    rng = np.random.default_rng(S * 7 + B)
+    y = rng.standard_normal((B, 1)).astype(np.float32)
+    t = rng.standard_normal((S, B, 32)).astype(np.float32)
+    yd, td = torch.from_numpy(y).cuda(), torch.from_numpy(t).cuda()
+    n = int(lib.nfn_posterior_workspace_doubles(B, 1, 32))
+    ws = _canary_ws(n)
+    out = torch.empty((B,), dtype=torch.float32, device="cuda")
+    osum = torch.empty((1,), dtype=torch.float64, device="cuda")
+    ids, k = _ids(C2)
+    rc = lib.nfn_posterior_lse_f32(yd.data_ptr(), 1, td.data_ptr(), B * 32, 32, S, B, 1, ctypes.cast(ids, ctypes.c_void_p),
+                                   k, 1, None, None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(), None)
+    _lib.check(rc, "posterior")
+    torch.cuda.synchronize()
+    _check_canary(ws, n, f"posterior S={S} B={B}")
+    got = out.cpu().numpy()
+    assert float(osum.item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)
+    idx = np.r_[0:64, rng.integers(0, B, 192), B - 64:B]
+    r64 = O.posterior_lse(y[idx], t[:, idx], C2, 1, True)
+    r32 = O.posterior_lse(y[idx], t[:, idx], C2, 1, True, dtype=np.float32)
+    assert (np.abs(got[idx] - r64) <= O.tolerance_bound(r64, r32)).all()
+
+
+@pytest.mark.parametrize("d,ft", [(20, ("radial", "radial", "affine")), (24, ("radial", "radial", "affine")),
+                                  (32, ("radial", "radial", "affine")), (17, ("affine", "affine", "affine")),
+                                  (8, ("affine",) + ("planar",) * 4 + ("radial",) * 4)])
+@pytest.mark.parametrize("B", [10000, 777])
+def test_group_partials_stay_in_workspace(d, ft, B, gpu):
+    """with 17 <= d <= 32 the 8-lane-group kernel's grid (B/32
+    workgroups) outgrew the partial slots (B/64)."""
+    from normalizingflownetwork_amd import _lib
+
+    lib = _lib.load()
+    P = O.total_param_size(ft, d, True)
+    assert P % 4 == 0
+    rng = np.random.default_rng(d * 1000 + B)
+    y = rng.standard_normal((B, d)).astype(np.float32)
+    t = (0.5 * rng.standard_normal((B, P))).astype(np.float32)
+    yd, td = torch.from_numpy(y).cuda(), torch.from_numpy(t).cuda()
+    n = int(lib.nfn_chain_workspace_doubles(B, d, P))
+    ws = _canary_ws(n)
+    out = torch.empty((B,), dtype=torch.float32, device="cuda")
+    osum = torch.empty((1,), dtype=torch.float64, device="cuda")
+    ids, k = _ids(ft)
+    rc = lib.nfn_chain_logprob_f32(yd.data_ptr(), d, td.data_ptr(), P, B, d, ctypes.cast(ids, ctypes.c_void_p), k, 1,
+                                   None, None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(), None)
+    _lib.check(rc, "chain")
+    torch.cuda.synchronize()
+    _check_canary(ws, n, f"chain d={d} B={B}")
+    got = out.cpu().numpy()
+    r64 = O.chain_log_prob(y, t, ft, d, True, np.float64)
+    r32 = O.chain_log_prob(y, t, ft, d, True, np.float32)
+    assert (np.abs(got - r64) <= O.tolerance_bound(r64, r32)).all()
+    assert float(osum.item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)
+    assert ws[1].item() == 0.0  # no non-finite values
+
+
+def _poison(y, rows_nan, rows_inf):
+    y = y.copy()
+    y[rows_nan, 0] = np.nan
+    y[rows_inf, 0] = np.inf
+    return y
+
+
+@pytest.mark.parametrize("name", ["c2_pr5_d1", "c3_apr_d8", "asym_pra_d3", "c1_nfn_radial2_d1"])
+def test_nonfinite_count_chain(name, gpu):
+    from normalizingflownetwork_amd import ops
+
+    g = load_golden(name)
+    B = g["y"].shape[0]
+    y = _poison(g["y"], [0, 5, B - 1], [7, B // 2])
+    lp, s, nf = ops.chain_log_prob(y, g["t"], g["flow_types"], g["d"], bool(g["trainable"]), want_nonfinite=True)
+    with np.errstate(all="ignore"):
+        ref = O.chain_log_prob(y, g["t"], g["flow_types"], g["d"], bool(g["trainable"]), np.float64)
+    n_ref = int((~np.isfinite(ref)).sum())
+    assert n_ref >= 5
+    assert int(nf.item()) == n_ref == int((~torch.isfinite(lp)).sum().item())
+    assert not np.isfinite(s.item())  # propagates, as the reference's .mean() does
+    # sum-only launch, and the pre-bound launcher's reduction
+    _, _, nf2 = ops.chain_log_prob(y, g["t"], g["flow_types"], g["d"], bool(g["trainable"]), want_values=False,
+                                   want_nonfinite=True)
+    assert int(nf2.item()) == n_ref
+    # clean input: zero
+    _, _, nf0 = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], g["d"], bool(g["trainable"]), want_nonfinite=True)
+    assert int(nf0.item()) == int((~np.isfinite(g["ref64"])).sum())
+
+
+def test_nonfinite_count_posterior_dense_launcher(gpu):
+    from normalizingflownetwork_amd import ops
+
+    gp = load_golden("posterior_s8_pr5_d1")
+    B = gp["y"].shape[0]
+    y = _poison(gp["y"], [1, 2], [3])
+    out, s, nf = ops.posterior_lse(y, gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"],
+                                   want_nonfinite=True)
+    assert int(nf.item()) == 3 == int((~torch.isfinite(out)).sum().item())
+    # fused Dense path (chain) and fused DenseVariational path (posterior)
+    rng = np.random.default_rng(3)
+    H, P = 16, 32
+    h = torch.from_numpy(rng.standard_normal((B, H)).astype(np.float32)).cuda()
+    W = torch.from_numpy((rng.standard_normal((H, P)) / 4).astype(np.float32)).cuda()
+    b = torch.zeros((P,), device="cuda")
+    yd = torch.from_numpy(y).cuda()
+    _, _, nfd = ops.chain_log_prob_dense(yd, h, W, b, C2, 1, True, want_nonfinite=True)
+    assert int(nfd.item()) == 3
+    hs = h.unsqueeze(0).expand(4, B, H).contiguous()
+    _, _, nfp = ops.posterior_lse_dense(yd, hs, W.unsqueeze(0).expand(4, H, P).contiguous(),
+                                        b.unsqueeze(0).expand(4, P).contiguous(), C2, 1, True, want_nonfinite=True)
+    assert int(nfp.item()) == 3
+    L = ops.ChainLauncher(yd, torch.from_numpy(load_golden("c2_pr5_d1")["t"][:B]).cuda(), C2, 1, True)
+    L.launch()
+    L.finish_sum()
+    assert int(L.nonfinite.item()) == 3
+
+
+def test_concurrent_streams_match_single_stream(gpu):
+    """calls in flight on two streams (each with its own workspace)
+    give the single-stream results bitwise."""
+    from normalizingflownetwork_amd import ops
+
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    B = 1 << 20
+    ys = [torch.randn((B, 1), generator=gen, device="cuda") for _ in range(2)]
+    ts = [torch.randn((B, 32), generator=gen, device="cuda") for _ in range(2)]
+    tp = [torch.randn((16, B // 16, 32), generator=gen, device="cuda") for _ in range(2)]
+    ref = [ops.chain_log_prob(ys[i], ts[i], C2, 1, True, want_sum=True) for i in range(2)]
+    pref = [ops.posterior_lse(ys[i][: B // 16], tp[i], C2, 1, True, want_sum=True) for i in range(2)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got, pgot = [None, None], [None, None]
+    for rep in range(3):
+        for i in range(2):
+            with torch.cuda.stream(streams[i]):
+                got[i] = ops.chain_log_prob(ys[i], ts[i], C2, 1, True, want_sum=True)
+                pgot[i] = ops.posterior_lse(ys[i][: B // 16], tp[i], C2, 1, True, want_sum=True)
+        torch.cuda.synchronize()
+        for i in range(2):
+            assert torch.equal(got[i][0], ref[i][0]) and torch.equal(got[i][1], ref[i][1])
+            assert torch.equal(pgot[i][0], pref[i][0]) and torch.equal(pgot[i][1], pref[i][1])
+
+
+def test_c4_global_batch_on_one_device(gpu):
+    """2^27 samples (C4's global batch) in one launch: t is 16 GiB, element offsets pass
+    2^31.  Samples spread over the whole batch (and the last rows) against the oracle;
+    the fused sum and the non-finite count against the returned values."""
+    from normalizingflownetwork_amd import ops
+
+    B, P = 1 << 27, 32
+    gen = torch.Generator(device="cuda").manual_seed(27)
+    y = torch.randn((B, 1), generator=gen, device="cuda")
+    t = torch.randn((B, P), generator=gen, device="cuda")
+    lp, s, nf = ops.chain_log_prob(y, t, C2, 1, True, want_nonfinite=True)
+    torch.cuda.synchronize()
+    fin = torch.isfinite(lp)
+    assert int(nf.item()) == int((~fin).sum().item())
+    if bool(fin.all()):
+        assert float(s.item()) == pytest.approx(float(lp.double().sum().item()), rel=1e-12)
+    idx = torch.cat([torch.randint(0, B, (3000,), generator=gen, device="cuda"),
+                     torch.arange((1 << 26) - 500, (1 << 26) + 500, device="cuda"),
+                     torch.arange(B - 600, B, device="cuda")])
+    yn, tn = y[idx].cpu().numpy(), t[idx].cpu().numpy()
+    r64 = O.chain_log_prob(yn, tn, C2, 1, True, np.float64)
+    r32 = O.chain_log_prob(yn, tn, C2, 1, True, np.float32)
+    got = lp[idx].cpu().numpy().astype(np.float64)
+    ok = np.isfinite(r64)
+    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    del t
+    torch.cuda.empty_cache()

@@ -14,7 +14,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from normalizingflownetwork_amd import ops  # noqa: E402
+from normalizingflownetwork_amd import _lib, ops  # noqa: E402
+
+_lib.use_diagnostic_build()  # the NFN_* tuning / ablation knobs live only in the NFN_DIAG build
 
 CFG = {
     "C2": (("planar", "radial") * 5, 1, 1 << 24, None),
