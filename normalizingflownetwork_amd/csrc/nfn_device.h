@@ -223,16 +223,20 @@ __device__ __forceinline__ float softplus_tf(float x) {
 }
 
 // Radial alpha = softplus(0.3 a - 2) (RadialFlow.py:24-27) feeds h = 1 / (alpha + r),
-// so it needs RELATIVE accuracy as alpha -> 0: in the fast form ln(1 + e) rounds to 0
-// once e < 2^-24 (alpha = 0, h = inf at z == gamma, where TF stays finite).  Below
-// x = -5 (e < 6.7e-3) use log1p(e) = e (1 - e (1/2 - e/3)), relative error < 1e-7.
+// so it needs RELATIVE accuracy as alpha -> 0: in the plain fast form ln(1 + e) rounds
+// to 0 once e < 2^-24 (alpha = 0, h = inf at z == gamma, where TF stays finite).  The
+// rounding error of u = 1 + e is recovered exactly (c = e - (u - 1)) and added back:
+// ln(1 + e) = ln(u) + c / u ~ ln(u) + c.  Three VALU ops, no select, no transcendental.
+__device__ __forceinline__ float softplus_acc_fast(float x, float e) {
+  const float u = 1.0f + e;
+  const float c = e - (u - 1.0f);
+  return fmaf(__builtin_amdgcn_logf(u), kLn2, fmaxf(x, 0.0f) + c);
+}
+
 template <bool FAST>
 __device__ __forceinline__ float softplus_alpha(float x) {
   if constexpr (FAST) {
-    const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
-    const float l = fmaf(__builtin_amdgcn_logf(1.0f + e), kLn2, fmaxf(x, 0.0f));
-    const float sr = e * fmaf(-e, fmaf(e, -1.0f / 3.0f, 0.5f), 1.0f);
-    return x < -5.0f ? sr : l;
+    return softplus_acc_fast(x, __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e));
   } else {
     return softplus_tf<false>(x);
   }

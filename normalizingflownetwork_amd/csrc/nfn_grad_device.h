@@ -183,10 +183,14 @@ __device__ __forceinline__ void base_bwd(const float (&z)[DM], float (&a)[DM], f
 // ---------------------------------------------------------------------------
 
 // softplus(x) and sigmoid(x) from e = e^{-|x|}: sigmoid = 1/(1+e) (x >= 0) or e/(1+e).
+template <bool ACC = false>
 __device__ __forceinline__ void sp_sig1(float x, float& sp, float& sg) {
   const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
   const float r = __builtin_amdgcn_rcpf(1.0f + e);
-  sp = fmaf(__builtin_amdgcn_logf(1.0f + e), kLn2, fmaxf(x, 0.0f));
+  if constexpr (ACC)
+    sp = softplus_acc_fast(x, e);
+  else
+    sp = fmaf(__builtin_amdgcn_logf(1.0f + e), kLn2, fmaxf(x, 0.0f));
   sg = x >= 0.0f ? r : e * r;
 }
 
@@ -242,8 +246,7 @@ __device__ __forceinline__ void radial1_bwd(float z, float& a, float p0, float p
   const float xa = fmaf(0.3f, p0, -2.0f);
   const float xb = fmaf(0.1f, p1, kLogExpm1One);
   float al, sga, spb, sgb;
-  sp_sig1(xa, al, sga);
-  al = xa < -5.0f ? softplus_alpha<true>(xa) : al;  // relative accuracy as alpha -> 0
+  sp_sig1<true>(xa, al, sga);  // relative accuracy as alpha -> 0 (softplus_alpha)
   sp_sig1(xb, spb, sgb);
   const float be = spb - 1.0f;
   const float dz = z - p2;
@@ -444,8 +447,7 @@ __device__ __forceinline__ void radial_gd_bwd(const float (&z)[DPL], float (&a)[
   const float xb = 0.1f * p[1] + kLogExpm1One;
   float al, sga, spb, sgb;
   if constexpr (FAST) {
-    sp_sig1(xa, al, sga);
-    al = xa < -5.0f ? softplus_alpha<true>(xa) : al;  // relative accuracy as alpha -> 0
+    sp_sig1<true>(xa, al, sga);  // relative accuracy as alpha -> 0 (softplus_alpha)
     sp_sig1(xb, spb, sgb);
   } else {
     al = softplus_tf<false>(xa);

@@ -336,6 +336,30 @@ def posterior_lse(y, t_draws, flow_types, d, trainable_base, y_mean=None, y_std=
     return (lse - np.log(dt.type(S))).astype(dt)
 
 
+def fp32_spread(y, t, flow_types, d, trainable_base, y_mean=None, y_std=None, n_perturbed=3, seed=0):
+    """The reference's own fp32 sensitivity per sample: the largest deviation from the
+    fp64 truth of the fp32 op-by-op mirror evaluated at the given inputs and at
+    ``n_perturbed`` copies whose inputs are moved by one random ulp (+-2^-23 relative).
+    One fp32 run of an ill-conditioned sample (a planar step with ``w.u_hat -> -1``,
+    ``PlanarFlow.py:49-53, 74-80``) can be luckily accurate; inputs indistinguishable at
+    fp32 precision show how far the reference's fp32 arithmetic really moves.  The same
+    construction as the backward's ``nfn_grad_oracle.fp32_spread``.  Returns
+    ``(ref64, spread32)``."""
+    ref64 = log_pdf(y, t, flow_types, d, trainable_base, y_mean, y_std, np.float64)
+    rng = np.random.default_rng(seed)
+    spread = np.zeros_like(ref64)
+    y32, t32 = np.asarray(y, np.float32), np.asarray(t, np.float32)
+    for k in range(n_perturbed + 1):
+        if k == 0:
+            yk, tk = y32, t32
+        else:
+            yk = (y32 * (1 + rng.integers(-1, 2, y32.shape) * 2.0 ** -23)).astype(np.float32)
+            tk = (t32 * (1 + rng.integers(-1, 2, t32.shape) * 2.0 ** -23)).astype(np.float32)
+        r32 = log_pdf(yk, tk, flow_types, d, trainable_base, y_mean, y_std, np.float32)
+        spread = np.maximum(spread, np.abs(r32.astype(np.float64) - ref64))
+    return ref64, spread
+
+
 # ---------------------------------------------------------------------------
 # Parity tolerance
 # ---------------------------------------------------------------------------

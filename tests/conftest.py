@@ -46,11 +46,12 @@ FLOW_FIXTURES = [f"flow_{f}_d{d}" for f in ("planar", "radial", "affine") for d 
 # Parity margins measured by the GPU tests (written at session end when non-empty).
 PARITY = []
 # A sample admitted only through the fp32-conditioning term of oracle.tolerance_bound
-# (|gpu - ref64| > 1e-5 max(1, |ref64|)) must still be within WIDEN_CAP x |ref32 - ref64|.
+# (|gpu - ref64| > 1e-5 max(1, |ref64|)) must still be within WIDEN_CAP x the reference's
+# fp32 sensitivity (oracle.fp32_spread where the check has the inputs, else |ref32 - ref64|).
 WIDEN_CAP = 2.0
 
 
-def record_parity(what, got, ref64, ref32, err, bound):
+def record_parity(what, got, ref64, ref32, err, bound, spread32=None):
     """Per check: the max of |gpu - ref64| / max(1, |ref64|); the max of |gpu - ref64| / |ref64|
     over |ref64| < 1; the samples admitted only through the fp32-conditioning widening, their
     count and max |gpu - ref64| / |ref32 - ref64|; the worst sample relative to its bound."""
@@ -71,6 +72,8 @@ def record_parity(what, got, ref64, ref32, err, bound):
         "widened_max_err_over_dev32": float((err[widened] / np.maximum(dev32[widened], 1e-300)).max())
         if widened.any() else None,
         "widened_max_err_over_base": float((err[widened] / base[widened]).max()) if widened.any() else None,
+        "widened_max_err_over_spread32": float((err[widened] / np.maximum(np.asarray(spread32)[widened], 1e-300)).max())
+        if (widened.any() and spread32 is not None) else None,
         "worst": {"idx": w, "got": float(np.ravel(got)[w]), "ref64": float(ref64.ravel()[w]),
                   "ref32": float(np.ravel(ref32)[w]), "err_over_bound": float(np.ravel(err)[w] / np.ravel(bound)[w])},
     })

@@ -35,7 +35,8 @@ nproc > "$OUT/nproc.txt"; lscpu > "$OUT/lscpu.txt" 2>&1 || true
 
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 480 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
+    testsx) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 240 python bench.py --steps 50 --warmup 10 ;;
     bench_nocpu) run bench_nocpu 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
@@ -55,6 +56,10 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o w -- \
         python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    dgrad) run bench_dense_grad 300 python bench.py --mode dense_grad --steps 20 --warmup 5 --cpu-seconds 8 ;;
+    prof_dgrad)
+      { cd /tmp; run rocprof_dgrad 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_dgrad" -o dgrad -- \
+        python3 "$ROOT/bench.py" --mode dense_grad --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
     grad) run bench_grad_c2 300 python bench.py --mode grad --steps 20 --warmup 5 --cpu-seconds 8 ;;
     grad_c3) run bench_grad_c3 300 python bench.py --mode grad --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
     prof_grad)
