@@ -331,7 +331,7 @@ def main():
             return
         s = launcher.finish_sum(sh)
         if native is not None:
-            native.allreduce_mean(s, B, sh, local_nonfinite=launcher.nonfinite)
+            native.allreduce_mean(launcher.sum2, B, sh)
         elif dist_on:
             i = nstep[0] % 2
             nstep[0] += 1

@@ -123,16 +123,18 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *   t          : (B or 1, P) rows at t_rowstride floats (0 = broadcast), P = nfn_total_param_size
  *   y_mean/y_std : (d,) device arrays or both NULL
  *   out_logp   : (B,) may be NULL when only the sum is wanted
- *   out_sum    : device double[1] or NULL — receives sum_b out_logp[b] (fp64 accumulation;
- *                non-finite values propagate, as in the reference's .mean())
+ *   out_sum    : device double[2] or NULL — receives {sum_b out_logp[b] (fp64 accumulation;
+ *                non-finite values propagate, as in the reference's .mean()), the number of
+ *                non-finite out_logp values}, finished inside the kernel by its last
+ *                workgroup (fixed summation order: bitwise deterministic; no extra launch)
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
+ *                ZERO-INITIALISED before its first use; every call leaves it reusable.
  *                Layout: workspace[0] = number n of per-workgroup pairs written,
- *                workspace[1] = number of non-finite out_logp values (written by the
- *                reduction, i.e. valid once out_sum is), workspace[2 + 2i] /
+ *                workspace[1] = the finishing ticket (0 between calls), workspace[2 + 2i] /
  *                workspace[3 + 2i] = workgroup i's fp64 partial sum / non-finite count.
  *                With out_sum == NULL and workspace != NULL only the pairs are written
  *                (finish with nfn_reduce_partials_f64).  One workspace per call in
- *                flight: two calls sharing one race.
+ *                flight: two calls in flight sharing one race.
  */
 int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
                               int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
@@ -207,11 +209,10 @@ int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride,
  * (deterministic). */
 int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream);
 
-/* Finishes a partials-only call: out_sum[0] = sum of the partial sums a chain /
- * posterior call left in `workspace`; the total non-finite count goes to workspace[1]
- * and, if out_nonfinite != NULL, to out_nonfinite[0] (a device double).  Fixed order:
- * bitwise deterministic. */
-int32_t nfn_reduce_partials_f64(double* workspace, double* out_sum, double* out_nonfinite, void* stream);
+/* Finishes a partials-only call: out_sum (device double[2]) := {sum of the partial sums,
+ * number of non-finite values} a chain / posterior call left in `workspace`.  The same
+ * fixed order as the in-kernel finish: bitwise identical to out_sum of the same call. */
+int32_t nfn_reduce_partials_f64(const double* workspace, double* out_sum, void* stream);
 
 /* Number of doubles of device workspace for nfn_posterior_lse_f32: the partials
  * block (as for the chain) followed by the draw-split region.  Passing a
@@ -223,7 +224,7 @@ int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P);
  * Bayesian posterior score per sample:
  *   out_lse[b] = logsumexp_s( logp(y_b | t[s, b]) [- sum log y_std] ) - log(S)
  *   t : S draws; draw s, sample b at t + s*t_drawstride + b*t_rowstride
- *   out_sum (nullable) receives sum_b out_lse[b] (fp64).
+ *   out_sum (nullable), workspace: as nfn_chain_logprob_f32 — {sum_b out_lse[b], non-finite count}.
  */
 int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
                               int64_t t_rowstride, int32_t S, int64_t B, int32_t d,
@@ -277,15 +278,16 @@ int32_t nfn_posterior_lse_dense_f32(const float* y, int64_t y_bstride, const flo
  *                        caller distributes to every rank (any channel).
  *   nfn_comm_init      : collective over all ranks; binds the CURRENT HIP device.
  *   nfn_allreduce_mean : sum_count (device double[3]) := sum over ranks of
- *                        {local_sum[0], local_count, local_nonfinite[0] (0 if NULL)};
- *                        mean_out (device double[1], nullable) := sum / count.
- *                        One 24-byte RCCL all-reduce.  Stream-ordered, no host sync.
+ *                        {local_sum[0], local_count, local_sum[1]}, where local_sum is a
+ *                        {sum, non-finite count} pair as out_sum returns it; mean_out
+ *                        (device double[1], nullable) := sum / count.  One 24-byte RCCL
+ *                        all-reduce.  Stream-ordered, no host sync.
  */
 int32_t nfn_comm_unique_id(uint8_t* id_out);
 int32_t nfn_comm_init(void** comm_out, int32_t nranks, const uint8_t* id, int32_t rank);
 int32_t nfn_comm_destroy(void* comm);
-int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, const double* local_nonfinite,
-                           double* sum_count, double* mean_out, void* stream);
+int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, double* sum_count,
+                           double* mean_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -24,7 +24,7 @@ SIGNATURES = {
     "nfn_last_error": (ctypes.c_char_p, []),
     "nfn_set_math_mode": (_c_int32, [_c_int32]),
     "nfn_reduce_sum_f64": (_c_int32, [_vp, _c_int64, _vp, _vp]),
-    "nfn_reduce_partials_f64": (_c_int32, [_vp, _vp, _vp, _vp]),
+    "nfn_reduce_partials_f64": (_c_int32, [_vp, _vp, _vp]),
     "nfn_param_size": (_c_int32, [_c_int32, _c_int32]),
     "nfn_total_param_size": (_c_int32, [_vp, _c_int32, _c_int32, _c_int32]),
     "nfn_chain_workspace_doubles": (_c_int64, [_c_int64, _c_int32, _c_int32]),
@@ -77,7 +77,7 @@ SIGNATURES = {
     "nfn_comm_unique_id": (_c_int32, [_vp]),
     "nfn_comm_init": (_c_int32, [ctypes.POINTER(_vp), _c_int32, _vp, _c_int32]),
     "nfn_comm_destroy": (_c_int32, [_vp]),
-    "nfn_allreduce_mean": (_c_int32, [_vp, _vp, _c_int64, _vp, _vp, _vp, _vp]),
+    "nfn_allreduce_mean": (_c_int32, [_vp, _vp, _c_int64, _vp, _vp, _vp]),
 }
 
 # Status codes (include/nfn.h)

@@ -146,7 +146,7 @@ int64_t partials_capacity(int64_t B, int P) {
   return (B + rows - 1) / rows;
 }
 
-// Doubles of the [count | non-finite | (sum, count) pairs] block.
+// Doubles of the [count | ticket | (sum, count) pairs] block.
 int64_t partials_doubles(int64_t B, int P) { return 2 + 2 * partials_capacity(B, P); }
 
 // Draw ranges per tile for the posterior: enough (64-row tile, range) units for
@@ -190,7 +190,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (B == 0) {
     if (out_sum) {
-      if (hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+      if (hipMemsetAsync(out_sum, 0, 2 * sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
     }
     return NFN_OK;
   }
@@ -204,7 +204,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   a.y_mean = y_mean;
   a.y_std = y_std;
   a.out = out;
-  a.partials = workspace ? workspace + 2 : nullptr;  // [count | non-finite | pairs]
+  a.partials = workspace ? workspace + 2 : nullptr;  // [count | ticket | pairs]
+  a.out_sum = workspace ? out_sum : nullptr;         // finished in-kernel by the last workgroup
   a.grid_cap = workspace ? partials_capacity(B, P) : 0;
   a.y_bstride = y_bstride;
   a.t_rowstride = t_rowstride;
@@ -276,7 +277,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
         int32_t rc0 = check_hip("posterior kernel launch");
         if (rc0 != NFN_OK) return rc0;
         nblk = (B + kMaxBlock - 1) / kMaxBlock;
-        launch_posterior_merge(fast, (const float2*)a.split_out, a.nsplit, S, B, out, workspace ? workspace + 2 : nullptr, s);
+        launch_posterior_merge(fast, (const float2*)a.split_out, a.nsplit, S, B, out, workspace ? workspace + 2 : nullptr,
+                               a.out_sum, s);
       }
     } else {
       if (fast) launch_persistent_fast(false, dm, Q, a, g.rows, lds_p, s, &nblk);
@@ -289,13 +291,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     const dim3 grid((unsigned)nblk), block((unsigned)g.threads);
     launch_tile(use_fast_math(), posterior, dm, a, grid, block, g.lds_bytes, s);
   }
-  int32_t rc = check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
-  if (rc != NFN_OK) return rc;
-  if (out_sum) {
-    launch_reduce_partials(workspace, out_sum, nullptr, s);
-    rc = check_hip("reduce_partials_kernel launch");
-  }
-  return rc;
+  return check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
 }
 
 int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B, int32_t d,
@@ -411,7 +407,7 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (B == 0) {
-    if (out_sum && hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+    if (out_sum && hipMemsetAsync(out_sum, 0, 2 * sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
     return NFN_OK;
   }
   if (!y || !h || !W) return fail(NFN_E_NULLPTR, "y, h or W is NULL");
@@ -423,6 +419,7 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   a.y_std = y_std;
   a.out = out;
   a.partials = workspace ? workspace + 2 : nullptr;
+  a.out_sum = workspace ? out_sum : nullptr;
   a.y_bstride = y_bstride;
   a.B = B;
   a.d = d;
@@ -444,13 +441,7 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   int64_t grid = 0;
   if (!launch_dense(use_fast_math(), dm_for(d), H / 4, da, lds, s, &grid))
     return fail(NFN_E_SHAPE, "no fused dense instance for this shape");
-  int32_t rc = check_hip("chain_dense_kernel launch");
-  if (rc != NFN_OK) return rc;
-  if (out_sum) {
-    launch_reduce_partials(workspace, out_sum, nullptr, s);
-    rc = check_hip("reduce_partials_kernel launch");
-  }
-  return rc;
+  return check_hip("chain_dense_kernel launch");
 }
 
 int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_drawstride,
@@ -479,7 +470,7 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (B == 0) {
-    if (out_sum && hipMemsetAsync(out_sum, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
+    if (out_sum && hipMemsetAsync(out_sum, 0, 2 * sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync");
     return NFN_OK;
   }
   if (!y || !h || !W) return fail(NFN_E_NULLPTR, "y, h or W is NULL");
@@ -491,6 +482,7 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   a.y_std = y_std;
   a.out = out;
   a.partials = workspace ? workspace + 2 : nullptr;
+  a.out_sum = workspace ? out_sum : nullptr;
   a.y_bstride = y_bstride;
   a.B = B;
   a.d = d;
@@ -511,13 +503,7 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   int64_t grid = 0;
   if (!launch_posterior_dense(use_fast_math(), dm_for(d), da, s, &grid))
     return fail(NFN_E_SHAPE, "no fused dense posterior instance for this shape");
-  int32_t rc = check_hip("posterior_dense_kernel launch");
-  if (rc != NFN_OK) return rc;
-  if (out_sum) {
-    launch_reduce_partials(workspace, out_sum, nullptr, s);
-    rc = check_hip("reduce_partials_kernel launch");
-  }
-  return rc;
+  return check_hip("posterior_dense_kernel launch");
 }
 
 constexpr int64_t kDenseGradMaxParts = 2048;  // per-workgroup partials (>= CUs x resident workgroups)
@@ -723,19 +709,19 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   (void)d;
   (void)P;
   if (B <= 0) return 0;
-  return partials_doubles(B, P);  // [count | non-finite | (sum, count) pairs]
+  return partials_doubles(B, P);  // [count | ticket | (sum, count) pairs]
 }
 
 int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
   if (B <= 0) return 0;
-  // [count | non-finite | pairs | draw-split region: (max, sum) float2 per (range, sample)]
+  // [count | ticket | pairs | draw-split region: (max, sum) float2 per (range, sample)]
   return partials_doubles(B, P) + (int64_t)posterior_split(B) * B;
 }
 
-int32_t nfn_reduce_partials_f64(double* workspace, double* out_sum, double* out_nonfinite, void* stream) {
+int32_t nfn_reduce_partials_f64(const double* workspace, double* out_sum, void* stream) {
   g_last_error.clear();
   if (!workspace || !out_sum) return fail(NFN_E_NULLPTR, "workspace or out_sum is NULL");
-  launch_reduce_partials(workspace, out_sum, out_nonfinite, reinterpret_cast<hipStream_t>(stream));
+  launch_reduce_partials(workspace, out_sum, reinterpret_cast<hipStream_t>(stream));
   return check_hip("reduce_partials_kernel launch");
 }
 

@@ -20,10 +20,10 @@ int32_t comm_fail(ncclResult_t r, const char* what) {
 }
 
 __global__ void pack_sum_count_kernel(const double* __restrict__ local_sum, double count,
-                                      const double* __restrict__ local_nf, double* __restrict__ sum_count) {
+                                      double* __restrict__ sum_count) {
   sum_count[0] = local_sum[0];
   sum_count[1] = count;
-  sum_count[2] = local_nf ? local_nf[0] : 0.0;
+  sum_count[2] = local_sum[1];
 }
 
 __global__ void finish_mean_kernel(const double* __restrict__ sum_count, double* __restrict__ mean) {
@@ -65,13 +65,13 @@ int32_t nfn_comm_destroy(void* comm) {
   return r == ncclSuccess ? NFN_OK : comm_fail(r, "ncclCommDestroy");
 }
 
-int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, const double* local_nonfinite,
-                           double* sum_count, double* mean_out, void* stream) {
+int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, double* sum_count,
+                           double* mean_out, void* stream) {
   if (!comm || !local_sum || !sum_count)
     return set_error(NFN_E_NULLPTR, "nfn_allreduce_mean: NULL comm, local_sum or sum_count");
   if (local_count < 0) return set_error(NFN_E_SHAPE, "nfn_allreduce_mean: negative local_count");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  pack_sum_count_kernel<<<1, 1, 0, s>>>(local_sum, (double)local_count, local_nonfinite, sum_count);
+  pack_sum_count_kernel<<<1, 1, 0, s>>>(local_sum, (double)local_count, sum_count);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NFN_E_HIP, hipGetErrorString(e));
   const ncclResult_t r = ncclAllReduce(sum_count, sum_count, 3, ncclFloat64, ncclSum,

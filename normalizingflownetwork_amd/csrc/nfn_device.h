@@ -76,6 +76,7 @@ struct ChainArgs {
   const float* y_std;
   float* out;
   double* partials;
+  double* out_sum;     // {sum, non-finite count} finished in-kernel by the last workgroup, or NULL
   int64_t y_bstride;
   int64_t t_rowstride;
   int64_t t_drawstride;
@@ -639,11 +640,52 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // TerminateOnNaN, BaseEstimator.py:29; score's .mean() silently returns -inf / NaN).
 __device__ __forceinline__ int nonfinite1(float v) { return __builtin_isfinite(v) ? 0 : 1; }
 
+// Fixed-order sum of n (sum, non-finite count) pairs by ONE workgroup of any size
+// (64..256 threads): virtual wave k in [0, kSumWaves) sums pairs 64 k + lane, + 256, ...
+// and is combined by a butterfly, the waves in order by thread 0 — so the in-kernel
+// finish and nfn_reduce_partials_f64 give bitwise-identical results.  `red` holds
+// 2 * kSumWaves doubles; contains a __syncthreads.  out[0] = sum, out[1] = count.
+constexpr int kSumWaves = 4;
+__device__ __forceinline__ void sum_pairs(const double* __restrict__ pairs, int64_t n, double* red, double* out) {
+  const int lane = threadIdx.x & 63, nw = (int)(blockDim.x >> 6), wid = (int)(threadIdx.x >> 6);
+  for (int k = wid; k < kSumWaves; k += nw) {
+    double s = 0.0, c = 0.0;
+    for (int64_t i = 64 * k + lane; i < n; i += 64 * kSumWaves) {
+      s += pairs[2 * i];
+      c += pairs[2 * i + 1];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_xor(s, off);
+      c += __shfl_xor(c, off);
+    }
+    if (lane == 0) {
+      red[2 * k] = s;
+      red[2 * k + 1] = c;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ts = 0.0, tc = 0.0;
+    for (int k = 0; k < kSumWaves; ++k) {
+      ts += red[2 * k];
+      tc += red[2 * k + 1];
+    }
+    out[0] = ts;
+    out[1] = tc;
+  }
+}
+
 // Workspace partials: pairs (sum, non-finite count) per workgroup at partials[2 blk],
 // partials[2 blk + 1]; the header partials[-2] (= workspace[0]) is the number of
-// pairs, partials[-1] (= workspace[1]) is filled by the reduction.  `red` holds
-// 2 * kMaxBlock / 64 doubles.  Contains a __syncthreads: call from every thread.
-__device__ __forceinline__ void write_partial(double* partials, double acc, int nf, double* red) {
+// pairs.  With out_sum, the LAST workgroup to finish (a ticket counter at
+// partials[-1] = workspace[1], zero before the call and left zero after it) sums every
+// pair in fixed order into out_sum = {sum, non-finite count}: no reduction launch.
+// The ticket is an agent-scope acq_rel vector atomic, so the pairs written on other
+// XCDs (other L2s) are visible to the finishing workgroup.  `red` holds
+// 2 * kMaxBlock / 64 doubles.  Contains __syncthreads: call from every thread.
+__device__ __forceinline__ void write_partial(double* partials, double acc, int nf, double* red,
+                                              double* out_sum) {
   double c = (double)nf;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -667,6 +709,21 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
     partials[2 * blockIdx.x + 1] = n;
     if (blockIdx.x == 0) partials[-2] = (double)gridDim.x;  // workspace header: number of pairs
   }
+  if (out_sum == nullptr) return;  // partials-only launch (nfn_reduce_partials_f64 finishes it)
+  unsigned* ticket = reinterpret_cast<unsigned*>(partials - 1);
+  int* flag = reinterpret_cast<int*>(red);
+  __syncthreads();  // red is free again
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0;
+  __syncthreads();
+  if (!last) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // every wave of the finishing workgroup
+  sum_pairs(partials, gridDim.x, red, out_sum);
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -695,7 +752,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
     lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
     if (a.out) a.out[b] = lp;
   }
-  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red);
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red, a.out_sum);
 }
 
 // Posterior: the same tile walk once per draw, with an online logsumexp over draws.
@@ -732,7 +789,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
     res = lse_finish<FAST>(m, acc, a.S);
     if (a.out) a.out[b0 + tid] = res;
   }
-  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red);
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red, a.out_sum);
 }
 
 // Persistent, software-pipelined version of the two kernels above (the hot path).
@@ -941,7 +998,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     }
   }
   if (a.partials && (!POST || nsp == 1)) {
-    write_partial(a.partials, acc, nfc, red);
+    write_partial(a.partials, acc, nfc, red, a.out_sum);
   }
 }
 
@@ -1056,7 +1113,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   }
   flush();
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red);
+    write_partial(a.partials, acc, nfc, red, a.out_sum);
   }
 }
 
@@ -1065,7 +1122,8 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
 template <bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2* __restrict__ parts, int nsplit,
                                                                      int S, int64_t B, float* __restrict__ out,
-                                                                     double* __restrict__ partials) {
+                                                                     double* __restrict__ partials,
+                                                                     double* __restrict__ out_sum) {
   __shared__ double red[2 * kMaxBlock / 64];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float res = 0.0f;
@@ -1091,7 +1149,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2
     }
     if (out) out[b] = res;
   }
-  if (partials) write_partial(partials, b < B ? (double)res : 0.0, b < B ? nonfinite1(res) : 0, red);
+  if (partials) write_partial(partials, b < B ? (double)res : 0.0, b < B ? nonfinite1(res) : 0, red, out_sum);
 }
 
 // ---------------------------------------------------------------------------
@@ -1412,7 +1470,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   }
   if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red);
+    write_partial(a.partials, acc, nfc, red, a.out_sum);
   }
 }
 
@@ -1515,7 +1573,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   }
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red);
+    write_partial(a.partials, acc, nfc, red, a.out_sum);
   }
 }
 

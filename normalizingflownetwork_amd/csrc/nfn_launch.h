@@ -89,9 +89,9 @@ void launch_sample(bool fast, int dm, const SampleArgs& sa, dim3 grid, dim3 bloc
 // nfn_grid.hip
 void launch_grid(bool fast, int dm, const GridArgs& ga, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_misc.hip
-void launch_reduce_partials(double* ws, double* out, double* out_nf, hipStream_t s);
+void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);
 void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,
-                            hipStream_t s);
+                            double* out_sum, hipStream_t s);
 
 }  // namespace nfn

@@ -8,6 +8,7 @@ There is no CPU fallback — without a GPU these raise ``RuntimeError``.
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Optional, Sequence
 
 import numpy as np
@@ -67,21 +68,33 @@ def total_param_size(flow_types: Sequence[str], n_dims: int, trainable_base: boo
     return sum(param_size(f, n_dims) for f in flow_types) + (2 * n_dims if trainable_base else 0)
 
 
+_workspaces: dict = {}
+_ws_lock = threading.Lock()
+
+
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
-    """A fresh workspace per call from torch's stream-aware caching allocator (cheap):
-    calls in flight on different streams or threads never share partials or the
-    posterior's split region.  ``ws[1]`` receives the call's non-finite count."""
-    return torch.empty(max(2, n_doubles), dtype=torch.float64, device=device)
+    """The zero-initialised workspace of the current (device, stream): calls are ordered on
+    their stream, so calls in flight on different streams never share partials, the
+    posterior's split region or the finishing ticket (which every call leaves at 0, so a
+    workspace is zeroed once, when it is created or grown)."""
+    key = (device.index, int(torch.cuda.current_stream(device).cuda_stream))
+    with _ws_lock:
+        ws = _workspaces.get(key)
+        if ws is None or ws.numel() < n_doubles:
+            ws = torch.zeros(max(2, n_doubles), dtype=torch.float64, device=device)
+            _workspaces[key] = ws
+        return ws
 
 
-def _with_nonfinite(out, osum, ws, want_nonfinite: bool):
-    """``(out, sum)`` or, with ``want_nonfinite``, ``(out, sum, nonfinite)`` where
-    ``nonfinite`` is a (1,) fp64 device tensor: the number of inf / NaN values among the
-    summed log-densities (counted by the kernel next to the partial sums; SURVEY.md §5,
+def _with_nonfinite(out, osum, want_nonfinite: bool):
+    """``(out, sum)`` or, with ``want_nonfinite``, ``(out, sum, nonfinite)``: ``osum`` is the
+    kernel's (2,) fp64 {sum, non-finite count}; ``nonfinite`` counts the inf / NaN values
+    among the summed log-densities (next to the partial sums in the kernel; SURVEY.md §5,
     the reference's ``TerminateOnNaN``, ``BaseEstimator.py:29``)."""
+    s = None if osum is None else osum[0:1]
     if not want_nonfinite:
-        return out, osum
-    return out, osum, ws[1:2]
+        return out, s
+    return out, s, osum[1:2]
 
 
 def _prep_2d(x, width: int, name: str, device) -> torch.Tensor:
@@ -125,7 +138,7 @@ def chain_log_prob(
         assert ym.numel() == n_dims and ys.numel() == n_dims
     want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
-    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    osum = torch.empty((2,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
     ws = _workspace(int(lib.nfn_chain_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
     ids, k = flow_ids(flow_types)
@@ -135,7 +148,7 @@ def chain_log_prob(
         _ptr(out), _ptr(osum), _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_chain_logprob_f32")
-    return _with_nonfinite(out, osum, ws, want_nonfinite)
+    return _with_nonfinite(out, osum, want_nonfinite)
 
 
 def chain_log_prob_grad(
@@ -307,7 +320,7 @@ def chain_log_prob_dense(
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
     want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
-    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    osum = torch.empty((2,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
     ws = _workspace(int(lib.nfn_chain_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
     ids, k = flow_ids(flow_types)
@@ -317,7 +330,7 @@ def chain_log_prob_dense(
         _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_chain_logprob_dense_f32")
-    return _with_nonfinite(out, osum, ws, want_nonfinite)
+    return _with_nonfinite(out, osum, want_nonfinite)
 
 
 def chain_log_prob_dense_grad(
@@ -435,7 +448,7 @@ def posterior_lse_dense(
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
     want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
-    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    osum = torch.empty((2,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
     ws = _workspace(int(lib.nfn_chain_workspace_doubles(B, n_dims, P)), dev) if want_sum else None
     ids, k = flow_ids(flow_types)
@@ -445,7 +458,7 @@ def posterior_lse_dense(
         _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_posterior_lse_dense_f32")
-    return _with_nonfinite(out, osum, ws, want_nonfinite)
+    return _with_nonfinite(out, osum, want_nonfinite)
 
 
 class DenseLauncher:
@@ -461,14 +474,15 @@ class DenseLauncher:
         assert dense_fusable(self.H, self.P, self.n_dims) and h.stride(1) == 1 and tuple(W.shape) == (self.H, self.P)
         self.y, self.h, self.W, self.b = y, h, W.contiguous(), b
         self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
-        self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
-        self.partials = torch.empty((max(2, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
+        self.sum2 = torch.zeros((2,), dtype=torch.float64, device=dev)  # {sum, non-finite}
+        self.sum = self.sum2[0:1]
+        self.partials = torch.zeros((max(2, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
                                     dtype=torch.float64, device=dev)
         self._ids, self._k = flow_ids(flow_types)
         self._args = (
             _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), self.H, _ptr(self.W), _ptr(b), self.B, self.n_dims,
             ctypes.cast(self._ids, ctypes.c_void_p), self._k, int(bool(trainable_base)), None, None, _ptr(self.out),
-            None, _ptr(self.partials),
+            _ptr(self.sum2), _ptr(self.partials),
         )
 
     def launch(self, stream: Optional[int] = None) -> None:
@@ -477,16 +491,13 @@ class DenseLauncher:
             _lib.check(rc, "nfn_chain_logprob_dense_f32")
 
     def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
-        rc = self.lib.nfn_reduce_partials_f64(_ptr(self.partials), _ptr(self.sum), None,
-                                              stream if stream is not None else _stream())
-        if rc != 0:
-            _lib.check(rc, "nfn_reduce_partials_f64")
+        """The launch's fp64 sum (finished inside the kernel: nothing to launch)."""
         return self.sum
 
     @property
     def nonfinite(self) -> torch.Tensor:
-        """(1,) fp64: non-finite values among the last reduced launch's log-densities."""
-        return self.partials[1:2]
+        """(1,) fp64: non-finite values among the last launch's log-densities."""
+        return self.sum2[1:2]
 
 
 class PosteriorDenseLauncher(DenseLauncher):
@@ -505,14 +516,15 @@ class PosteriorDenseLauncher(DenseLauncher):
         self.y, self.h, self.W = y, h, W.contiguous()
         self.b = None if b is None else b.contiguous()
         self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
-        self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
-        self.partials = torch.empty((max(2, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
+        self.sum2 = torch.zeros((2,), dtype=torch.float64, device=dev)  # {sum, non-finite}
+        self.sum = self.sum2[0:1]
+        self.partials = torch.zeros((max(2, int(self.lib.nfn_chain_workspace_doubles(self.B, self.n_dims, self.P))),),
                                     dtype=torch.float64, device=dev)
         self._ids, self._k = flow_ids(flow_types)
         self._args = (
             _ptr(y), _row_stride(y), _ptr(h), int(h.stride(0)), int(h.stride(1)), self.H, _ptr(self.W),
             self.H * self.P, _ptr(self.b), self.P, self.S, self.B, self.n_dims, ctypes.cast(self._ids, ctypes.c_void_p),
-            self._k, int(bool(trainable_base)), None, None, _ptr(self.out), None, _ptr(self.partials),
+            self._k, int(bool(trainable_base)), None, None, _ptr(self.out), _ptr(self.sum2), _ptr(self.partials),
         )
 
     def launch(self, stream: Optional[int] = None) -> None:
@@ -634,7 +646,7 @@ def posterior_lse(
         ys = as_device_f32(y_std, dev).reshape(-1).contiguous()
     want_sum = want_sum or want_nonfinite
     out = torch.empty((B,), dtype=torch.float32, device=dev) if want_values else None
-    osum = torch.empty((1,), dtype=torch.float64, device=dev) if want_sum else None
+    osum = torch.empty((2,), dtype=torch.float64, device=dev) if want_sum else None
     lib = _lib.load()
     # the workspace also enables the draw split (more parallelism for small B)
     ws = _workspace(int(lib.nfn_posterior_workspace_doubles(B, n_dims, P)), dev)
@@ -645,7 +657,7 @@ def posterior_lse(
         _ptr(out), _ptr(osum), _ptr(ws), _stream(),
     )
     _lib.check(rc, "nfn_posterior_lse_f32")
-    return _with_nonfinite(out, osum, ws, want_nonfinite)
+    return _with_nonfinite(out, osum, want_nonfinite)
 
 
 def set_math_mode(mode: str) -> str:
@@ -662,11 +674,12 @@ class ChainLauncher:
     buffers (the benchmark / serving loop): all validation and pointer
     marshalling happens once; ``launch()`` is a single C-ABI call.
 
-    ``launch()`` writes ``out`` (B,) and the per-workgroup fp64 partial sums;
-    ``finish_sum()`` reduces the partials into ``sum`` (1,) fp64."""
+    ``launch()`` writes ``out`` (B,) and ``sum2`` = {fp64 sum, non-finite count}, finished
+    in the kernel by its last workgroup (``sum`` is ``sum2[0:1]``)."""
 
     def __init__(self, y: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
-                 trainable_base: bool, write_values: bool = True, draws: Optional[int] = None):
+                 trainable_base: bool, write_values: bool = True, draws: Optional[int] = None,
+                 fused_sum: bool = True):
         self.lib = _lib.load()
         dev = y.device
         self.n_dims = int(n_dims)
@@ -681,10 +694,12 @@ class ChainLauncher:
             self.B = max(int(y.shape[0]), int(t.shape[0]))
         self.y, self.t = y, t
         self.out = torch.empty((self.B,), dtype=torch.float32, device=dev) if write_values else None
-        self.sum = torch.zeros((1,), dtype=torch.float64, device=dev)
+        self.sum2 = torch.zeros((2,), dtype=torch.float64, device=dev)  # {sum, non-finite}
+        self.sum = self.sum2[0:1]
         fn_ws = self.lib.nfn_posterior_workspace_doubles if self.posterior else self.lib.nfn_chain_workspace_doubles
         self.n_partials = int(fn_ws(self.B, self.n_dims, self.P))
-        self.partials = torch.empty((max(2, self.n_partials),), dtype=torch.float64, device=dev)
+        self.partials = torch.zeros((max(2, self.n_partials),), dtype=torch.float64, device=dev)
+        self.fused_sum = fused_sum
         self._ids, self._k = flow_ids(flow_types)
         self._ids_p = ctypes.cast(self._ids, ctypes.c_void_p)
         self._trainable = int(bool(trainable_base))
@@ -692,16 +707,17 @@ class ChainLauncher:
             self._args = (
                 _ptr(y), _row_stride(y), _ptr(t), int(t.stride(0)), 0 if t.shape[1] == 1 else int(t.stride(1)),
                 int(draws), self.B, self.n_dims, self._ids_p, self._k, self._trainable, None, None,
-                _ptr(self.out), None, _ptr(self.partials),
+                _ptr(self.out), _ptr(self.sum2) if fused_sum else None, _ptr(self.partials),
             )
             self._fn = self.lib.nfn_posterior_lse_f32
         else:
             self._args = (
                 _ptr(y), _row_stride(y), _ptr(t), _row_stride(t), self.B, self.n_dims, self._ids_p, self._k,
-                self._trainable, None, None, _ptr(self.out), None, _ptr(self.partials),
+                self._trainable, None, None, _ptr(self.out), _ptr(self.sum2) if fused_sum else None,
+                _ptr(self.partials),
             )
             self._fn = self.lib.nfn_chain_logprob_f32
-        self._sum_args = (_ptr(self.partials), _ptr(self.sum), None)
+        self._sum_args = (_ptr(self.partials), _ptr(self.sum2))
 
     def launch(self, stream: Optional[int] = None) -> None:
         rc = self._fn(*self._args, stream if stream is not None else _stream())
@@ -709,15 +725,19 @@ class ChainLauncher:
             _lib.check(rc, "fused chain launch")
 
     def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
-        rc = self.lib.nfn_reduce_partials_f64(*self._sum_args, stream if stream is not None else _stream())
-        if rc != 0:
-            _lib.check(rc, "nfn_reduce_partials_f64")
+        """``sum`` (1,) fp64 of the last launch: finished inside the kernel by default; with
+        ``fused_sum=False`` the launch writes only the partials and this reduces them
+        (``nfn_reduce_partials_f64``, the same summation order and bits)."""
+        if not self.fused_sum:
+            rc = self.lib.nfn_reduce_partials_f64(*self._sum_args, stream if stream is not None else _stream())
+            if rc != 0:
+                _lib.check(rc, "nfn_reduce_partials_f64")
         return self.sum
 
     @property
     def nonfinite(self) -> torch.Tensor:
-        """(1,) fp64: non-finite values among the last reduced launch's log-densities."""
-        return self.partials[1:2]
+        """(1,) fp64: non-finite values among the last launch's log-densities."""
+        return self.sum2[1:2]
 
 
 class GradLauncher:

@@ -101,20 +101,16 @@ class NativeComm:
         self.sum_count = torch.zeros((3,), dtype=torch.float64, device=dev)  # sum, count, non-finite
         self.mean = torch.zeros((1,), dtype=torch.float64, device=dev)
 
-    def allreduce_mean(self, local_sum: torch.Tensor, local_count: int, stream=None,
-                       local_nonfinite: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """``{sum, count, non-finite}`` summed over ranks into ``self.sum_count``; returns
-        the device scalar ``sum / count`` (``self.mean``).  Stream-ordered."""
+    def allreduce_mean(self, local_sum: torch.Tensor, local_count: int, stream=None) -> torch.Tensor:
+        """``local_sum`` = the kernel's (2,) fp64 {sum, non-finite count} (``out_sum``);
+        ``{sum, count, non-finite}`` summed over ranks into ``self.sum_count``; returns the
+        device scalar ``sum / count`` (``self.mean``).  Stream-ordered."""
         from . import _lib
 
-        assert local_sum.dtype == torch.float64 and local_sum.is_cuda
+        assert local_sum.dtype == torch.float64 and local_sum.is_cuda and local_sum.numel() == 2
         if stream is None:
             stream = torch.cuda.current_stream().cuda_stream
-        nf_ptr = None
-        if local_nonfinite is not None:
-            assert local_nonfinite.dtype == torch.float64 and local_nonfinite.is_cuda
-            nf_ptr = local_nonfinite.data_ptr()
-        _lib.check(self._lib.nfn_allreduce_mean(self.handle, local_sum.data_ptr(), int(local_count), nf_ptr,
+        _lib.check(self._lib.nfn_allreduce_mean(self.handle, local_sum.data_ptr(), int(local_count),
                                                 self.sum_count.data_ptr(), self.mean.data_ptr(), int(stream)),
                    "nfn_allreduce_mean")
         return self.mean

@@ -17,10 +17,10 @@ def test_native_comm_single_rank_mean(gpu):
 
     comm = NativeComm()
     try:
-        s = torch.tensor([12.5], dtype=torch.float64, device=gpu)
+        s = torch.tensor([12.5, 2.0], dtype=torch.float64, device=gpu)  # {sum, non-finite count}
         m = comm.allreduce_mean(s, 5)
         torch.cuda.synchronize()
-        assert comm.sum_count.tolist() == [12.5, 5.0, 0.0]
+        assert comm.sum_count.tolist() == [12.5, 5.0, 2.0]
         assert m.item() == 2.5
     finally:
         comm.close()
@@ -36,11 +36,11 @@ def test_native_comm_mean_log_prob_matches_oracle(gpu):
     rng = np.random.default_rng(7)
     y = rng.standard_normal((B, d)).astype(np.float32)
     t = rng.standard_normal((B, P)).astype(np.float32)
-    _, s = ops.chain_log_prob(torch.from_numpy(y).to(gpu), torch.from_numpy(t).to(gpu), ft, d, True,
-                              want_values=False, want_sum=True)
+    _, s, nf = ops.chain_log_prob(torch.from_numpy(y).to(gpu), torch.from_numpy(t).to(gpu), ft, d, True,
+                                  want_values=False, want_nonfinite=True)
     comm = NativeComm()
     try:
-        m = comm.allreduce_mean(s.reshape(1), B).item()
+        m = comm.allreduce_mean(torch.cat([s, nf]), B).item()
     finally:
         comm.close()
     ref = float(np.mean(O.chain_log_prob(y, t, ft, d, True)))

@@ -291,7 +291,7 @@ def test_full_size_properties(cfg, gpu):
     lpp, _ = ops.chain_log_prob(y[perm], t[perm], ft, d, True)
     assert torch.equal(lpp, lp1[perm])
     # the partials-only launch + nfn_reduce_partials_f64 gives the same sum
-    L = ops.ChainLauncher(y, t, ft, d, True, write_values=False)
+    L = ops.ChainLauncher(y, t, ft, d, True, write_values=False, fused_sum=False)
     L.launch()
     assert torch.equal(L.finish_sum(), s1)
     # 4096 random samples (spread over the whole batch) against the oracle

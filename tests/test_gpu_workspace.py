@@ -32,7 +32,10 @@ def _ids(ft):
 
 
 def _canary_ws(n):
+    """The workspace the library asks for (zero-initialised: the finishing ticket) followed
+    by 64 sentinel doubles."""
     ws = torch.full((n + 64,), SENTINEL, dtype=torch.float64, device="cuda")
+    ws[:n] = 0.0
     return ws
 
 
@@ -55,7 +58,7 @@ def test_posterior_split_stays_in_workspace(S, B, gpu):
     n = int(lib.nfn_posterior_workspace_doubles(B, 1, 32))
     ws = _canary_ws(n)
     out = torch.empty((B,), dtype=torch.float32, device="cuda")
-    osum = torch.empty((1,), dtype=torch.float64, device="cuda")
+    osum = torch.empty((2,), dtype=torch.float64, device="cuda")
     ids, k = _ids(C2)
     rc = lib.nfn_posterior_lse_f32(yd.data_ptr(), 1, td.data_ptr(), B * 32, 32, S, B, 1, ctypes.cast(ids, ctypes.c_void_p),
                                    k, 1, None, None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(), None)
@@ -63,7 +66,8 @@ def test_posterior_split_stays_in_workspace(S, B, gpu):
     torch.cuda.synchronize()
     _check_canary(ws, n, f"posterior S={S} B={B}")
     got = out.cpu().numpy()
-    assert float(osum.item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)
+    assert float(osum[0].item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)
+    assert int(ws[1].item()) == 0  # the finishing ticket is left at zero
     idx = np.r_[0:64, rng.integers(0, B, 192), B - 64:B]
     r64 = O.posterior_lse(y[idx], t[:, idx], C2, 1, True)
     r32 = O.posterior_lse(y[idx], t[:, idx], C2, 1, True, dtype=np.float32)
@@ -89,7 +93,7 @@ def test_group_partials_stay_in_workspace(d, ft, B, gpu):
     n = int(lib.nfn_chain_workspace_doubles(B, d, P))
     ws = _canary_ws(n)
     out = torch.empty((B,), dtype=torch.float32, device="cuda")
-    osum = torch.empty((1,), dtype=torch.float64, device="cuda")
+    osum = torch.empty((2,), dtype=torch.float64, device="cuda")
     ids, k = _ids(ft)
     rc = lib.nfn_chain_logprob_f32(yd.data_ptr(), d, td.data_ptr(), P, B, d, ctypes.cast(ids, ctypes.c_void_p), k, 1,
                                    None, None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(), None)
@@ -103,9 +107,10 @@ def test_group_partials_stay_in_workspace(d, ft, B, gpu):
     fin = np.isfinite(r64)  # an affine scale 1 + t of 0 is a legitimate -inf log-density
     assert (np.abs(got[fin] - r64[fin]) <= O.tolerance_bound(r64[fin], r32[fin])).all()
     assert (~np.isfinite(got[~fin])).all()
-    assert ws[1].item() == float((~np.isfinite(got)).sum())  # the non-finite count
+    assert osum[1].item() == float((~np.isfinite(got)).sum())  # the non-finite count
+    assert int(ws[1].item()) == 0  # the finishing ticket is left at zero
     if fin.all():
-        assert float(osum.item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)
+        assert float(osum[0].item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)
 
 
 def _poison(y, rows_nan, rows_inf):
