@@ -265,14 +265,27 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
       // to fill the chip; needs the split region of the workspace
       // (the split region holds posterior_split(B) ranges; never more are used)
       int nsplit = workspace ? std::min(posterior_split(B), S) : 1;
-      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(env_int("NFN_POST_SPLIT", 1), nsplit);
+      // d = 1, fast math, contiguous rows: posterior_wave1_kernel (draw-inner buffer
+      // pipeline); it needs a split only when there are fewer tiles than resident waves
+      const bool pw1 = fast && d == 1 && wave && a.nt && (Q == 2 || Q == 4 || Q == 8 || Q == 16) &&
+                       t_rowstride * 256 < ((int64_t)1 << 31) && y_bstride * 256 < ((int64_t)1 << 31) &&
+                       env_int("NFN_POST_WAVE1", 1) != 0;
+      if (pw1) {
+        const int64_t resident = (int64_t)cu_count() * posterior_wave1_wgs_per_cu() * (kMaxBlock / 64);
+        nsplit = (int)std::min<int64_t>(nsplit, std::max<int64_t>(1, (resident + nblk - 1) / nblk));
+      }
+      if (env_int("NFN_POST_SPLIT", 0) > 0) nsplit = std::min(env_int("NFN_POST_SPLIT", 1), std::min(posterior_split(B), S));
       a.nsplit = nsplit;
       a.dps = (S + nsplit - 1) / nsplit;
       a.nsplit = (S + a.dps - 1) / a.dps;  // no empty ranges (<= nsplit)
       a.split_out = reinterpret_cast<float2*>(workspace + partials_doubles(B, P));
       if (a.nsplit > 1) a.grid_cap = 0;  // partials come from the merge kernel
-      if (fast) launch_persistent_fast(true, dm, Q, a, g.rows, lds_p, s, &nblk);
-      else launch_persistent_precise(true, dm, Q, a, g.rows, lds_p, s, &nblk);
+      if (pw1)
+        launch_posterior_wave1(Q, a, lds_p, s, &nblk);
+      else if (fast)
+        launch_persistent_fast(true, dm, Q, a, g.rows, lds_p, s, &nblk);
+      else
+        launch_persistent_precise(true, dm, Q, a, g.rows, lds_p, s, &nblk);
       if (a.nsplit > 1) {
         int32_t rc0 = check_hip("posterior kernel launch");
         if (rc0 != NFN_OK) return rc0;

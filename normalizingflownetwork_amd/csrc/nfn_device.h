@@ -51,6 +51,7 @@ constexpr float kLn2 = 0.69314718055994531f;
 constexpr float kLog2e = 1.44269504088896341f;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // 16-byte load of a parameter-row piece; NT = non-temporal (streamed once).
 template <bool NT>
@@ -646,13 +647,19 @@ __device__ __forceinline__ int nonfinite1(float v) { return __builtin_isfinite(v
 // finish and nfn_reduce_partials_f64 give bitwise-identical results.  `red` holds
 // 2 * kSumWaves doubles; contains a __syncthreads.  out[0] = sum, out[1] = count.
 constexpr int kSumWaves = 4;
+template <bool ATOMIC = false>
 __device__ __forceinline__ void sum_pairs(const double* __restrict__ pairs, int64_t n, double* red, double* out) {
   const int lane = threadIdx.x & 63, nw = (int)(blockDim.x >> 6), wid = (int)(threadIdx.x >> 6);
   for (int k = wid; k < kSumWaves; k += nw) {
     double s = 0.0, c = 0.0;
     for (int64_t i = 64 * k + lane; i < n; i += 64 * kSumWaves) {
-      s += pairs[2 * i];
-      c += pairs[2 * i + 1];
+      if constexpr (ATOMIC) {  // agent-coherent loads: pairs written by workgroups on other XCDs
+        s += __hip_atomic_load(pairs + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c += __hip_atomic_load(pairs + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        s += pairs[2 * i];
+        c += pairs[2 * i + 1];
+      }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -681,8 +688,10 @@ __device__ __forceinline__ void sum_pairs(const double* __restrict__ pairs, int6
 // pairs.  With out_sum, the LAST workgroup to finish (a ticket counter at
 // partials[-1] = workspace[1], zero before the call and left zero after it) sums every
 // pair in fixed order into out_sum = {sum, non-finite count}: no reduction launch.
-// The ticket is an agent-scope acq_rel vector atomic, so the pairs written on other
-// XCDs (other L2s) are visible to the finishing workgroup.  `red` holds
+// Only the pairs cross workgroups, so they are written and read as agent-scope
+// atomics (coherent across the XCDs' separate L2s) and ordered before the ticket by a
+// vmcnt(0) wait: no release / acquire fence, which would write back / invalidate the
+// whole L2 in every workgroup.  The ticket is a vector atomic.  `red` holds
 // 2 * kMaxBlock / 64 doubles.  Contains __syncthreads: call from every thread.
 __device__ __forceinline__ void write_partial(double* partials, double acc, int nf, double* red,
                                               double* out_sum) {
@@ -705,8 +714,8 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
       s += red[2 * w];
       n += red[2 * w + 1];
     }
-    partials[2 * blockIdx.x] = s;
-    partials[2 * blockIdx.x + 1] = n;
+    __hip_atomic_store(partials + 2 * blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partials + 2 * blockIdx.x + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0) partials[-2] = (double)gridDim.x;  // workspace header: number of pairs
   }
   if (out_sum == nullptr) return;  // partials-only launch (nfn_reduce_partials_f64 finishes it)
@@ -714,15 +723,15 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
   int* flag = reinterpret_cast<int*>(red);
   __syncthreads();  // red is free again
   if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pair has reached the coherence point
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag[0] = prev == gridDim.x - 1;
   }
   __syncthreads();
   const bool last = flag[0] != 0;
   __syncthreads();
   if (!last) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // every wave of the finishing workgroup
-  sum_pairs(partials, gridDim.x, red, out_sum);
+  sum_pairs<true>(partials, gridDim.x, red, out_sum);
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1115,6 +1124,137 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   if (a.partials) {
     write_partial(a.partials, acc, nfc, red, a.out_sum);
   }
+}
+
+// d = 1 Bayesian posterior (config C5) with chain_wave1_kernel's memory pipeline.  A
+// wave owns (tile, draw range) units — the 64 samples of a tile through draws
+// [sb, se) — and walks them DRAW-INNER: every (unit, draw) step hands its prefetched
+// rows (draw s of the tile: one contiguous 64 x P block of t (S, B, P)) to LDS behind
+// one counted wait, issues the NEXT step's rows (draw s + 1, or the next unit's first
+// draw) and y through buffer descriptors bounded at B, and stores the previous unit's
+// result, before the chain and the online logsumexp run on the current draw.  Every
+// step issues the same loads and one store (an empty descriptor except right after a
+// unit ends), so the pipeline is straight-line code with exact counted waits.  With
+// nsplit == 1 (enough tiles for every resident wave: C5 at 2^17 samples) a unit is a
+// whole tile, its score leaves once and there is no merge pass; otherwise units write
+// (max, scaled sum) pairs for posterior_merge_kernel.
+template <int Q, bool PACKED>
+__global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[2 * kMaxBlock / 64];
+  constexpr int RSTEP = 64 / Q;
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int LS = a.lds_stride;
+  const int64_t rs = a.t_rowstride, ds = a.t_drawstride;
+  const int r0 = lane / Q, c4 = lane % Q;
+  float* tl = lds + wid * 64 * LS;
+  const int l0 = r0 * LS + 4 * c4;
+  const int S = a.S, nsp = a.nsplit, dps = a.dps;
+  const int64_t ntiles = a.ntiles;
+  // units (tile, range) are visited as tile-major (tile, rg) pairs advanced by the
+  // grid stride without 64-bit divisions: stride = (ut tiles, ur ranges)
+  const int wstride = (int)(gridDim.x * (blockDim.x >> 6));
+  const int ut = wstride / nsp, ur = wstride - ut * nsp;
+  const int w0 = (int)(blockIdx.x * (blockDim.x >> 6)) + wid;
+  int64_t tile = w0 / nsp;
+  int rg = w0 - (int)tile * nsp;
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int toff = (r0 * (int)rs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)rs * 4;
+  const float logS = f_log<true>((float)S);
+
+  float4 buf[Q];
+  float ybuf;
+  // rows of draw s of tile `tl_`, and its y; tiles past the end issue empty descriptors
+  auto issue = [&](int64_t tl_, int s) {
+    const int64_t b0 = tl_ * 64;
+    const int64_t nr = tl_ < ntiles ? min((int64_t)64, a.B - b0) : 0;
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const auto rt = tile_rsrc(a.t + (nr > 0 ? s * ds + b0c * rs : 0), nr > 0 ? ((nr - 1) * rs + a.P) * 4 : 0);
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+  };
+
+  double acc_sum = 0.0;
+  int nfc = 0;
+  // the previous unit's result: log_prob (nsplit == 1) or its (max, scaled sum) pair
+  const __amdgpu_buffer_rsrc_t empty_r = tile_rsrc(a.out, 0);
+  __amdgpu_buffer_rsrc_t pend_r = empty_r;
+  float pend_v = 0.0f, pend_m = 0.0f;
+  auto flush = [&]() {
+    if (nsp == 1)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+    else
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(pend_m, pend_v)), pend_r,
+                                            lane * 8, 0, kNT);
+  };
+  issue(tile, rg * dps);
+  flush();
+  while (tile < ntiles) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = min((int64_t)64, a.B - b0);
+    const int sb = rg * dps, se = min(S, sb + dps);
+    // the next unit
+    int rgn = rg + ur;
+    int64_t tilen = tile + ut;
+    if (rgn >= nsp) {
+      rgn -= nsp;
+      tilen += 1;
+    }
+    float m = -INFINITY, lacc = 0.0f, z0 = 0.0f;
+    for (int s = sb; s < se; ++s) {
+      if (a.prio) __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        float* dst = tl + l0 + k * RSTEP * LS;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
+      if (s == sb) z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+      wave_lds_sync();
+      if (s + 1 < se)
+        issue(tile, s + 1);
+      else
+        issue(tilen, rgn * dps);
+      flush();
+      pend_r = empty_r;
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      const float lp = eval_chain1_fast<PACKED>(z0, tl + lane * LS, a) - corr;
+      lse_push<true>(m, lacc, lp);
+      wave_lds_sync();  // this draw's LDS reads done before the next draw's writes
+    }
+    if (nsp == 1) {
+      const float res = ((m == -INFINITY || m != m) ? m : m + f_log<true>(lacc)) - logS;
+      if (lane < nr) {
+        acc_sum += (double)res;
+        nfc += nonfinite1(res);
+      }
+      pend_v = res;
+      pend_r = tile_rsrc(a.out ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+    } else {
+      pend_m = m;
+      pend_v = lacc;
+      pend_r = tile_rsrc(a.split_out + (int64_t)rg * a.B + b0, nr * 8);
+    }
+    tile = tilen;
+    rg = rgn;
+  }
+  flush();
+  if (a.partials && nsp == 1) write_partial(a.partials, acc_sum, nfc, red, a.out_sum);
 }
 
 // Combines the per-range (max, scaled sum) pairs of a draw-split posterior:

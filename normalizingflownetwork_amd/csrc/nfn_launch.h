@@ -55,6 +55,9 @@ bool launch_persistent_fast(bool post, int dm, int Q, const ChainArgs& a, int T,
                             int64_t* grid);
 bool launch_persistent_precise(bool post, int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s,
                                int64_t* grid);
+// nfn_persistent.hip (fast-math unit): d = 1 posterior on the wave1 pipeline, Q in {2, 4, 8, 16}
+void launch_posterior_wave1(int Q, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid);
+int posterior_wave1_wgs_per_cu();
 // nfn_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance
 bool launch_group_fast(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
                        int64_t* grid);

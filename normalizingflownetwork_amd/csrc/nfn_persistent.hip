@@ -85,9 +85,36 @@ void launch_p_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream
   }
 }
 
+#if NFN_FAST
+template <int Q>
+void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = (a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? posterior_wave1_kernel<Q, true>
+                                                                : posterior_wave1_kernel<Q, false>;
+  const int64_t units = a.ntiles * a.nsplit;
+  const int64_t grid = cap_grid(std::min<int64_t>((units + 3) / 4, (int64_t)cu_count() * posterior_wave1_wgs_per_cu()), a);
+  *grid_out = grid;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+}
+#endif
+
 }  // namespace
 
 #if NFN_FAST
+// Resident workgroups per CU of posterior_wave1_kernel (4 waves each).
+int posterior_wave1_wgs_per_cu() {
+  const int w = env_int("NFN_WG_PER_CU", 0);
+  return w > 0 ? w : 2;
+}
+
+void launch_posterior_wave1(int Q, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid) {
+  switch (Q) {
+    case 2: launch_pw1<2>(a, lds, s, grid); break;
+    case 4: launch_pw1<4>(a, lds, s, grid); break;
+    case 8: launch_pw1<8>(a, lds, s, grid); break;
+    default: launch_pw1<16>(a, lds, s, grid); break;
+  }
+}
+
 bool launch_persistent_fast(bool post, int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s,
                             int64_t* grid) {
 #else

@@ -377,11 +377,14 @@ def test_radial_tiny_alpha_at_center(d, math_mode):
     t = (0.3 * rng.standard_normal((B, P))).astype(np.float32)
     # block of flow_types[0] is last (reversed layout): [a, b, gamma(d)]
     a_col, g0 = P - (d + 2), P - d
-    t[:, a_col] = np.linspace(-400.0, -20.0, B, dtype=np.float32)  # x = 0.3 a - 2 in [-122, -8]
+    # x = 0.3 a - 2 in [-42.8, -8]: the plain fast softplus rounded alpha to 0 below
+    # x = -16.6; below x = -44 the reference's own fp32 h' = (-1/y)/y overflows at r = 0
+    # (RadialFlow.py:63-66) and its log-density is NaN there too
+    t[:, a_col] = np.linspace(-136.0, -20.0, B, dtype=np.float32)
     t[:, g0:] = y  # z_0 == gamma: r = 0
     ref64 = O.chain_log_prob(y, t, ft, d, True, np.float64)
     ref32 = O.chain_log_prob(y, t, ft, d, True, np.float32)
-    assert np.isfinite(ref64).all()
+    assert np.isfinite(ref64).all() and np.isfinite(ref32).all()
     lp, _ = ops.chain_log_prob(y, t, ft, d, True)
     lp = lp.cpu().numpy()
     assert np.isfinite(lp).all(), f"{int((~np.isfinite(lp)).sum())} non-finite"

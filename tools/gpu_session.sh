@@ -75,6 +75,8 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write_grad 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_grad" -o w -- \
         python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    finish) run finish 300 python tools/microbench.py finish ;;
+    c5micro) run c5micro 300 python tools/microbench.py c5 ;;
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
     debugnf) run debugnf 300 python tools/debug_nonfinite.py C3 ;;
     mem) run mem 300 python tools/microbench.py mem ;;

@@ -258,8 +258,44 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
                           "evals_per_s": B / ms * 1e3, "rounds_ms": times[k]}), flush=True)
 
 
+def run_finish(cfgs=("C2", "C5", "C3"), reps=30, rounds=4):
+    """In-kernel finish of the fp64 sum (last-workgroup ticket) vs partials + the separate
+    reduce kernel, whole step (launch + finish) timed with events on the launch stream."""
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    for cfg in cfgs:
+        ft, d, B, S = CFG[cfg]
+        P = ops.total_param_size(ft, d, True)
+        gen = torch.Generator(device="cuda").manual_seed(1)
+        y = torch.randn((B, d), generator=gen, device="cuda")
+        t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device="cuda")
+        Ls = {"fused": ops.ChainLauncher(y, t, ft, d, True, draws=S, fused_sum=True),
+              "partials+reduce": ops.ChainLauncher(y, t, ft, d, True, draws=S, fused_sum=False)}
+        steps = {k: (lambda L=L: (L.launch(sh), L.finish_sum(sh))) for k, L in Ls.items()}
+        prewarm(steps["fused"])
+        times = {k: [] for k in steps}
+        for _ in range(rounds):
+            for k, fn in steps.items():
+                for _ in range(3):
+                    fn()
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+                for e0, e1 in evs:
+                    e0.record(stream)
+                    fn()
+                    e1.record(stream)
+                torch.cuda.synchronize()
+                times[k].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+        sums = {k: L.sum2.tolist() for k, L in Ls.items()}
+        for k in steps:
+            print(json.dumps({"cfg": cfg, "mode": "finish", "variant": k, "ms": float(np.median(times[k])),
+                              "rounds_ms": times[k], "sum_nonfinite": sums[k]}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "finish":
+        run_finish()
+        return
     if which[0] == "dgrad":
         run_dense_grad()
         return
@@ -329,16 +365,18 @@ def main():
                         {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                         {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}])
         return
-    if which[0] == "c5":  # posterior: occupancy x draw split of the generic persistent kernel
-        v = [{"name": "auto", "env": {}},
-             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
-             {"name": "split2", "env": {"NFN_POST_SPLIT": 2}}, {"name": "split8", "env": {"NFN_POST_SPLIT": 8}},
-             {"name": "split16", "env": {"NFN_POST_SPLIT": 16}},
-             {"name": "wg2_split8", "env": {"NFN_WG_PER_CU": 2, "NFN_POST_SPLIT": 8}},
-             {"name": "wg3_split8", "env": {"NFN_WG_PER_CU": 3, "NFN_POST_SPLIT": 8}},
-             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
-             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
-             {"name": "auto_b", "env": {}}]
+    if which[0] == "c5":  # posterior: posterior_wave1_kernel (default) vs the generic persistent kernel
+        G = {"NFN_POST_WAVE1": 0}
+        v = [{"name": "pw1", "env": {}},
+             {"name": "generic", "env": dict(G)},
+             {"name": "pw1_wg3", "env": {"NFN_WG_PER_CU": 3}}, {"name": "pw1_wg4", "env": {"NFN_WG_PER_CU": 4}},
+             {"name": "pw1_wg1", "env": {"NFN_WG_PER_CU": 1}},
+             {"name": "pw1_split2", "env": {"NFN_POST_SPLIT": 2}},
+             {"name": "pw1_split4_wg4", "env": {"NFN_POST_SPLIT": 4, "NFN_WG_PER_CU": 4}},
+             {"name": "pw1_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "pw1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "generic_split2", "env": dict(G, NFN_POST_SPLIT=2)},
+             {"name": "pw1_b", "env": {}}, {"name": "generic_b", "env": dict(G)}]
         run("C5", v)
         return
     if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
@@ -415,16 +453,18 @@ def main():
         for cfg in which[1:] or ["C2", "C1"]:
             run(cfg, v)
         return
-    if which[0] == "c5":  # posterior: occupancy x draw split of the generic persistent kernel
-        v = [{"name": "auto", "env": {}},
-             {"name": "wg2", "env": {"NFN_WG_PER_CU": 2}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
-             {"name": "split2", "env": {"NFN_POST_SPLIT": 2}}, {"name": "split8", "env": {"NFN_POST_SPLIT": 8}},
-             {"name": "split16", "env": {"NFN_POST_SPLIT": 16}},
-             {"name": "wg2_split8", "env": {"NFN_WG_PER_CU": 2, "NFN_POST_SPLIT": 8}},
-             {"name": "wg3_split8", "env": {"NFN_WG_PER_CU": 3, "NFN_POST_SPLIT": 8}},
-             {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
-             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
-             {"name": "auto_b", "env": {}}]
+    if which[0] == "c5":  # posterior: posterior_wave1_kernel (default) vs the generic persistent kernel
+        G = {"NFN_POST_WAVE1": 0}
+        v = [{"name": "pw1", "env": {}},
+             {"name": "generic", "env": dict(G)},
+             {"name": "pw1_wg3", "env": {"NFN_WG_PER_CU": 3}}, {"name": "pw1_wg4", "env": {"NFN_WG_PER_CU": 4}},
+             {"name": "pw1_wg1", "env": {"NFN_WG_PER_CU": 1}},
+             {"name": "pw1_split2", "env": {"NFN_POST_SPLIT": 2}},
+             {"name": "pw1_split4_wg4", "env": {"NFN_POST_SPLIT": 4, "NFN_WG_PER_CU": 4}},
+             {"name": "pw1_noprio", "env": {"NFN_PRIO": 0}},
+             {"name": "pw1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "generic_split2", "env": dict(G, NFN_POST_SPLIT=2)},
+             {"name": "pw1_b", "env": {}}, {"name": "generic_b", "env": dict(G)}]
         run("C5", v)
         return
     if which[0] == "group1":  # C3: branch-free buffer pipeline vs the generic group kernel
