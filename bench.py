@@ -164,8 +164,14 @@ def cpu_baseline(kind: str, cfg: str, H: int = 16, seconds: float = 8.0) -> dict
     one_evals, one_el = _cpu_worker((kind, cfg, total, 22, H, seconds))
     rows = max(64, total // n)
     ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's HIP state is inherited
-    with ctx.Pool(n) as pool:
+    pool = ctx.Pool(n)
+    try:
         res = pool.map(_cpu_worker, [(kind, cfg, rows, 22 + i, H, seconds) for i in range(n)])
+        pool.close()  # workers exit on their own (the context manager's terminate() SIGTERMs them)
+        pool.join()
+    except BaseException:
+        pool.terminate()
+        raise
     pooled = sum(e / el for e, el in res)
     unit_rows = "(draw, sample) pairs" if S is not None else "samples"
     what = {"forward": "numpy fp32 op-by-op chain", "dense": "numpy fp32 GEMM + op-by-op chain",
@@ -492,7 +498,7 @@ def main():
                 metric = f"DenseVariational(H={H})->posterior (draw, sample) evals/sec (whole node), {args.config}"
         else:
             kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel",
-                           "C5": "chain_persistent_kernel + posterior_merge_kernel"}[args.config]
+                           "C5": "posterior_wave1_kernel"}[args.config]
             metric = ("log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"
                       if args.config == "C2" else f"log_prob evals/sec (whole node), {args.config}")
         line = {
