@@ -487,7 +487,8 @@ def main():
             kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group1_kernel"
             metric = f"log_prob backward evals/sec (whole node), {args.config}"
         elif args.mode == "dense_grad":
-            kernel_name = "chain_dense_grad_kernel + sum_partials_kernel"
+            kernel_name = ("chain_dense1_grad_kernel" if d == 1 and H in (16, 32) else "chain_dense_grad_kernel") + \
+                " + sum_partials_kernel"
             metric = f"Dense(H={H})->log_prob backward evals/sec (whole node), {args.config}"
         elif args.mode == "dense":
             if S is None:
@@ -545,6 +546,11 @@ def main():
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
+            # fused Dense modes: the fp32 MFMA work per launch (t = hW, and for the backward
+            # dh = dt W^T, dW = h^T dt) against the 157.3 TF/s fp32 matrix peak
+            "mfma": None if not dense_mode else {
+                "tflops": (3 if grad_mode else 1) * 2.0 * B * H * P * (1 if S is None else S) / (kern_ms * 1e-3) / 1e12,
+                "peak": 157.3},
             "mean_log_prob": mean_ll,
             "nonfinite_log_prob": nonfinite,
             "unfused_ms": unfused_ms,

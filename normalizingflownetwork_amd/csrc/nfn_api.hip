@@ -534,6 +534,7 @@ int32_t run_dense_grad(const float* y, int64_t y_bstride, const float* h, int64_
   DenseArgs& da = g.da;
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMMs + streaming alone
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");

@@ -17,6 +17,7 @@ namespace nfn {
 namespace {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
 template <int DM, bool FAST, int MH, int NN>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradArgs g) {
@@ -227,19 +228,285 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradAr
   (void)HP;
 }
 
-// grad_W | grad_b = the sum of the per-workgroup partials, one thread per element,
-// workgroups in order (fp64 accumulation, deterministic)
-__global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, int nparts, int n,
-                                                           float* __restrict__ gW, float* __restrict__ gb, int nW) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double s = 0.0;
-  for (int k = 0; k < nparts; ++k) s += (double)part[(int64_t)k * n + i];
-  if (i < nW) {
-    if (gW) gW[i] = (float)s;
-  } else if (gb) {
-    gb[i - nW] = (float)s;
+// d = 1, fast math, H = 16 MH (MH in {1, 2}), P <= 16 NN: the same backward with
+// every operand placed for the matrix cores and chain_dense1_kernel's memory pipeline.
+// Per 64-sample wave tile (all MFMAs v_mfma_f32_16x16x4_f32, exact fp32):
+//   * h arrives by b128 buffer loads (lane (am, ak): h[16 mt + am][16 j + 4 ak .. + 3])
+//     and goes to LDS (row stride SH = H + 4: conflict-free b128 writes), to be read
+//     back as the A fragments of t = h W (in chain_dense1_kernel's hidden-unit order:
+//     t is bitwise the forward kernel's) and, transposed, as those of dW = h^T dt
+//     (contraction over samples in the order s = 16 kq + 4 ak + i, so that dt is read
+//     as b128), kept in registers across the chain; the W fragments of both GEMMs
+//     that read W (t = h W, dh^T = W dt^T) stay in registers for the whole launch;
+//   * t = h W + b leaves the matrix cores as b128 writes into a column-major t tile
+//     (stride kCS, overlaying the dead h rows); the chain backward runs per lane
+//     (grad1_packed on the column stride), turning t into dt in place;
+//   * dh^T = W dt^T (contraction over p in the order 16 (ks/4) + 4 ak + ks % 4: the
+//     two 16-lane halves of each ds_read_b32 group land on disjoint banks) — each lane
+//     then holds 4 consecutive hidden units of one sample: dh leaves as b128 stores;
+//   * dW += h^T dt, with db's column sums taken from the same b128 dt reads (VALU
+//     adds, lanes of one column combined once at the end).
+// Per wave LDS: the t tile ((P + 2) columns, the packed reverse pass reads up to two
+// past the last block) and the flow inputs z_k.  Every workgroup writes one partial
+// [dW | db], summed across waves in wave order: bitwise deterministic.
+template <int MH, int NN>
+__global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradArgs g) {
+  const DenseArgs& da = g.da;
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  constexpr int H = 16 * MH;
+  constexpr int QH = 4 * MH;
+  constexpr int SH = H + 4;  // h rows in LDS: 16-byte aligned, == 4 mod 8 (see above)
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwave = blockDim.x >> 6;
+  const int P = a.P;
+  const int K = a.prog.K;
+  const int wfl = dense1_grad_wave_floats(P, SH, K);
+  float* tl = lds + wid * wfl;  // t / dt tile, column-major; the h rows overlay it
+  float* hl = tl;
+  float* zh = tl + (P + 2) * kCS + lane;
+  const int am = lane & 15, ak = lane >> 4;
+
+  // W fragments: t GEMM B[k = hidden(ks)][n = p] and dh GEMM A[m = hidden][k = p(ks)]
+  float wB[QH][NN], wA[MH][4 * NN], bn[NN];
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    const int p = 16 * nt + am;
+    bn[nt] = (p < P && da.bias) ? da.bias[p] : 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks) wB[ks][nt] = p < P ? da.W[(4 * ks + ak) * P + p] : 0.0f;
   }
+#pragma unroll
+  for (int mh = 0; mh < MH; ++mh)
+#pragma unroll
+    for (int ks = 0; ks < 4 * NN; ++ks) {
+      const int p = 16 * (ks >> 2) + 4 * ak + (ks & 3);
+      wA[mh][ks] = p < P ? da.W[(16 * mh + am) * P + p] : 0.0f;
+    }
+
+  const int64_t hs = da.h_rowstride;
+  const int64_t ghs = g.gh_rowstride;
+  const int64_t ntiles = a.ntiles;
+  const int64_t u0 = (int64_t)blockIdx.x * nwave + wid;
+  const int64_t ustep = (int64_t)gridDim.x * nwave;
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const bool trainable = a.trainable != 0;
+  const uint32_t types = a.prog.types[0];
+  // loop-invariant byte offsets (the host guarantees 64 rows span < 2 GiB)
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int hoff = (am * (int)hs + 4 * ak) * 4;      // + mt * 16 rows + j * 16 floats
+  const int hmt = 16 * (int)hs * 4;
+  const int ghoff = (am * (int)ghs + 4 * ak) * 4;    // dh: row 16 mt + am, hidden 16 mh + 4 ak
+  const int ghmt = 16 * (int)ghs * 4;
+
+  float4 hb[4][MH];
+  float ybuf, gbuf;
+  auto issue = [&](int64_t tile) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const auto rg = tile_rsrc(g.g_out ? g.g_out + b0c : a.y, g.g_out ? nr * 4 : 0);
+    gbuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lane * 4, 0, 0));
+    const auto rh = tile_rsrc(da.h + b0c * hs, nr > 0 ? ((nr - 1) * hs + H) * 4 : 0);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < MH; ++j)
+        hb[mt][j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, mt * hmt + 64 * j, kNT));
+  };
+
+  f32x4v dw[MH][NN];
+  float db[NN];
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    db[nt] = 0.0f;
+#pragma unroll
+    for (int mh = 0; mh < MH; ++mh) dw[mh][nt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+
+  issue(u0);
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    // 1. h rows -> LDS (row-major); read back: the A fragments of t = h W (hidden units
+    // in chain_dense1_kernel's order, so t is bitwise the forward kernel's) and, transposed,
+    // those of dW (kept in registers across the chain)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < MH; ++j)
+        *reinterpret_cast<float4*>(hl + (16 * mt + am) * SH + 16 * j + 4 * ak) = hb[mt][j];
+    const float z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+    const float gl = g.g_out ? gbuf : 1.0f;
+    wave_lds_sync();
+    issue(tile + ustep);  // the next tile's loads (hb is free once in LDS)
+    float av[4][QH], hA[MH][16];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < QH; ++ks) av[mt][ks] = hl[(16 * mt + am) * SH + 4 * ks + ak];
+#pragma unroll
+    for (int mh = 0; mh < MH; ++mh)
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) hA[mh][ks] = hl[(16 * (ks >> 2) + 4 * ak + (ks & 3)) * SH + 16 * mh + am];
+    wave_lds_sync();  // every h read done before the t tile overwrites the rows
+    // 2. t = h W + b
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) {
+      f32x4v acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][ks], wB[ks][nt], acc[mt], 0, 0, 0);
+      if (16 * nt + am < P) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          *reinterpret_cast<f32x4v*>(tl + (16 * nt + am) * kCS + 16 * mt + 4 * ak) = acc[mt] + bn[nt];
+      }
+    }
+    wave_lds_sync();
+    // 3. the chain forward + reverse per lane: the t column entries become g * d logp / d t
+    float adj, z = z0;
+    const float lp = grad1_packed<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
+    if (nr < 64 && lane >= nr) {  // rows past B carry no gradient
+      for (int p = 0; p < P; ++p) tl[p * kCS + lane] = 0.0f;
+    }
+    {
+      const auto ro = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, lp), ro, lane * 4, 0, kNT);
+      const auto rdy = tile_rsrc(g.grad_y && nr > 0 ? g.grad_y + b0 : g.grad_y, g.grad_y ? nr * 4 : 0);
+      const float gy = norm ? f_div<true>(adj, ystd) : adj;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gy), rdy, lane * 4, 0, kNT);
+    }
+    wave_lds_sync();
+    // 4. dh^T = W dt^T: lane (am, ak) ends with dh[16 mt + am][16 mh + 4 ak .. + 3]
+    {
+      const auto rdh = tile_rsrc(g.grad_h && nr > 0 ? g.grad_h + b0 * ghs : g.grad_h,
+                                 g.grad_h && nr > 0 ? ((nr - 1) * ghs + H) * 4 : 0);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        float bv[4 * NN];
+#pragma unroll
+        for (int ks = 0; ks < 4 * NN; ++ks) {
+          const int p = 16 * (ks >> 2) + 4 * ak + (ks & 3);
+          bv[ks] = p < P ? tl[p * kCS + 16 * mt + am] : 0.0f;
+        }
+#pragma unroll
+        for (int mh = 0; mh < MH; ++mh) {
+          f32x4v acc = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int ks = 0; ks < 4 * NN; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[mh][ks], bv[ks], acc, 0, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc), rdh, ghoff, mt * ghmt + 64 * mh, kNT);
+        }
+      }
+    }
+    // 5. dW += h^T dt (contraction over the tile's samples), db += the same dt values
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) {
+      const bool col = 16 * nt + am < P;
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) {
+        f32x4v q = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+        if (col) q = *reinterpret_cast<const f32x4v*>(tl + (16 * nt + am) * kCS + 16 * kq + 4 * ak);
+        db[nt] += (q[0] + q[1]) + (q[2] + q[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int mh = 0; mh < MH; ++mh)
+            dw[mh][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(hA[mh][4 * kq + i], q[i], dw[mh][nt], 0, 0, 0);
+      }
+    }
+    wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
+  }
+  if (g.part == nullptr) return;  // no grad_W / grad_b requested (uniform: every thread returns)
+  // db: the four lanes of a column (ak = 0..3) combined in a fixed order
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    db[nt] += __shfl_xor(db[nt], 16);
+    db[nt] += __shfl_xor(db[nt], 32);
+  }
+  // each wave's [dW | db] into its own LDS region, then summed in wave order
+  const int nWb = H * P + P;
+  __syncthreads();
+  float* mine = lds + wid * wfl;
+#pragma unroll
+  for (int mh = 0; mh < MH; ++mh)
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hr = 16 * mh + 4 * ak + i, p = 16 * nt + am;  // C layout: row 4 ak + i, column am
+        if (p < P) mine[hr * P + p] = dw[mh][nt][i];
+      }
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt)
+    if (ak == 0 && 16 * nt + am < P) mine[H * P + 16 * nt + am] = db[nt];
+  __syncthreads();
+  float* out = g.part + (int64_t)blockIdx.x * nWb;
+  for (int i = tid; i < nWb; i += blockDim.x) {
+    float s = lds[i];
+    for (int w = 1; w < nwave; ++w) s += lds[w * wfl + i];
+    out[i] = s;
+  }
+}
+
+// grad_W | grad_b = the sum of the per-workgroup partials (fp64, deterministic): a
+// workgroup owns 64 consecutive elements (lane = element, coalesced rows of the
+// partials); its 16 waves take the partials w, w + 16, ... and are combined in wave order
+__global__ void __launch_bounds__(1024) sum_partials_kernel(const float* __restrict__ part, int nparts, int n,
+                                                            float* __restrict__ gW, float* __restrict__ gb, int nW) {
+  __shared__ double red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (i < n) {
+#pragma unroll 4
+    for (int k = w; k < nparts; k += 16) s += (double)part[(int64_t)k * n + i];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || i >= n) return;
+  double t = red[0][lane];
+  for (int v = 1; v < 16; ++v) t += red[v][lane];
+  if (i < nW) {
+    if (gW) gW[i] = (float)t;
+  } else if (gb) {
+    gb[i - nW] = (float)t;
+  }
+}
+
+template <int MH, int NN>
+int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
+  auto kfn = chain_dense1_grad_kernel<MH, NN>;
+  const size_t lds = (size_t)4 * dense1_grad_wave_floats(g.da.c.P, 16 * MH + 4, g.da.c.prog.K) * sizeof(float);
+  int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);
+  grid = std::max<int64_t>(1, std::min<int64_t>(grid, max_parts));
+  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, g);
+  return grid;
+}
+
+template <int MH>
+int64_t launch_dg1_n(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
+  switch ((g.da.c.P + 15) / 16) {
+    case 1: return launch_dg1<MH, 1>(g, max_parts, s);
+    case 2: return launch_dg1<MH, 2>(g, max_parts, s);
+    case 3: return launch_dg1<MH, 3>(g, max_parts, s);
+    case 4: return launch_dg1<MH, 4>(g, max_parts, s);
+  }
+  return 0;
 }
 
 template <int DM, bool FAST, int MH, int NN>
@@ -277,11 +544,19 @@ int64_t launch_dg_dm(int dm, const DenseGradArgs& g, size_t lds, int64_t max_par
 }  // namespace
 
 int64_t launch_dense_grad(bool fast, int dm, const DenseGradArgs& g, size_t lds, int64_t max_parts, hipStream_t s) {
+  const ChainArgs& a = g.da.c;
+  const int H = g.da.H;
+  if (fast && a.d == 1 && a.prog.K <= 16 && (H == 16 || H == 32) && a.P <= 64 &&
+      g.da.h_rowstride * 256 < ((int64_t)1 << 31) && g.gh_rowstride * 256 < ((int64_t)1 << 31) &&
+      a.y_bstride * 256 < ((int64_t)1 << 31) && (reinterpret_cast<uintptr_t>(g.grad_h) & 15) == 0 &&
+      (g.gh_rowstride & 3) == 0 && env_int("NFN_DENSE1_GRAD", 1) != 0 &&
+      (size_t)4 * dense1_grad_wave_floats(a.P, H + 4, a.prog.K) * sizeof(float) <= (size_t)160 * 1024)
+    return H == 16 ? launch_dg1_n<1>(g, max_parts, s) : launch_dg1_n<2>(g, max_parts, s);
   return fast ? launch_dg_dm<true>(dm, g, lds, max_parts, s) : launch_dg_dm<false>(dm, g, lds, max_parts, s);
 }
 
 void launch_sum_partials(const float* part, int64_t nparts, int n, float* gW, float* gb, int nW, hipStream_t s) {
-  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, (int)nparts, n,
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, s, part, (int)nparts, n,
                      gW, gb, nW);
 }
 

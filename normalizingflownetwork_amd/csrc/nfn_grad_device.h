@@ -211,7 +211,10 @@ __device__ __forceinline__ void radial1_z(float& z, float a0, float b0, float g)
   z = fmaf(ab * __builtin_amdgcn_rcpf(alpha + fabsf(dz)), dz, z);
 }
 
-// (p0, p1, p2): the flow's parameters (already read); `p`: where its gradient goes.
+// (p0, p1, p2): the flow's parameters (already read); `p`: where its gradient goes
+// (ST floats between consecutive parameters: 1 = row-major tile, the fused Dense
+// backward's column-major tile uses its padded column stride).
+template <int ST = 1>
 __device__ __forceinline__ void planar1_bwd(float z, float& a, float p0, float p1, float p2, float* p, float gl) {
   const float u = p0;
   const float w = p1 + 1.0f;
@@ -237,11 +240,12 @@ __device__ __forceinline__ void planar1_bwd(float z, float& a, float p0, float p
   const float wGn = w * G * rn;
   const float k1 = (sg - 1.0f) * wGn;
   p[0] = G * (fmaf(sg * w, w, 1e-9f) * rn);
-  p[1] = fmaf(z, Ss, fmaf(hpd, uh, fmaf(cn, G, fmaf(-2.0f * cn * wGn, w, k1 * u))));
-  p[2] = Ss;
+  p[ST] = fmaf(z, Ss, fmaf(hpd, uh, fmaf(cn, G, fmaf(-2.0f * cn * wGn, w, k1 * u))));
+  p[2 * ST] = Ss;
   a = fmaf(w, Ss, a);
 }
 
+template <int ST = 1>
 __device__ __forceinline__ void radial1_bwd(float z, float& a, float p0, float p1, float p2, float* p, float gl) {
   const float xa = fmaf(0.3f, p0, -2.0f);
   const float xb = fmaf(0.1f, p1, kLogExpm1One);
@@ -262,47 +266,51 @@ __device__ __forceinline__ void radial1_bwd(float z, float& a, float p0, float p
   const float hH = hh * H;
   const float sg = sign0(dz);
   p[0] = 0.3f * sga * g_al;
-  p[1] = 0.1f * sgb * al * g_ab;
-  p[2] = fmaf(hH, sg, -ab * h * a);
+  p[ST] = 0.1f * sgb * al * g_ab;
+  p[2 * ST] = fmaf(hH, sg, -ab * h * a);
   a = fmaf(fmaf(ab, h, 1.0f), a, -hH * sg);
 }
 
+template <int ST = 1>
 __device__ __forceinline__ void affine1_bwd(float z, float& a, float p0, float p1, float* p, float gl) {
   (void)p0;
   const float sc = 1.0f + p1;
   p[0] = a;
-  p[1] = fmaf(z, a, gl * __builtin_amdgcn_rcpf(sc));
+  p[ST] = fmaf(z, a, gl * __builtin_amdgcn_rcpf(sc));
   a *= sc;
 }
 
+template <int ST = 1>
 __device__ __forceinline__ void flow1_bwd(int id, float z, float& a, const float (&pv)[3], float* p, float gl) {
   if (id == NFN_FLOW_PLANAR)
-    planar1_bwd(z, a, pv[0], pv[1], pv[2], p, gl);
+    planar1_bwd<ST>(z, a, pv[0], pv[1], pv[2], p, gl);
   else if (id == NFN_FLOW_RADIAL)
-    radial1_bwd(z, a, pv[0], pv[1], pv[2], p, gl);
+    radial1_bwd<ST>(z, a, pv[0], pv[1], pv[2], p, gl);
   else
-    affine1_bwd(z, a, pv[0], pv[1], p, gl);
+    affine1_bwd<ST>(z, a, pv[0], pv[1], p, gl);
 }
 
 // d = 1, fast math, chains of <= 16 flows with the packed program (types 2 bits
 // per flow; offsets by scalar arithmetic: no scalar-memory loads inside the
 // loops, whose lgkmcnt(0) waits would drain the pipelined LDS reads).  Both
 // passes read the NEXT flow's parameters (and, in reverse, its input z) from LDS
-// before evaluating the current flow.
+// before evaluating the current flow.  ST: floats between a sample's consecutive
+// parameters (see planar1_bwd).
+template <int ST = 1>
 __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, int zs, uint32_t types, int K, int P,
                                               bool trainable, float gl, bool want_lp, float& adj) {
   float l2 = 0.0f;
   int id = (int)(types & 3u);
   int off = max(P - size1(id), 0);
   float pc[3];
-  if (K > 0) read3c(pc, row, off);
+  if (K > 0) read3c<ST>(pc, row, off);
 #pragma unroll 1
   for (int k = 0; k < 16; ++k) {
     if (k < K) {
       const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
       const int offn = max(off - size1(idn), 0);
       float pn[3];
-      read3c(pn, row, offn);
+      read3c<ST>(pn, row, offn);
       zh[k * zs] = z;
       if (want_lp) {
         l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
@@ -320,17 +328,17 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
       pc[2] = pn[2];
     }
   }
-  const float lp = want_lp ? base1_fast(z, row, trainable) + l2 * kLn2 : 0.0f;
+  const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
   float a1;
   if (trainable) {
     float sps, sgs;
-    sp_sig1(kLogExpm1One + 0.1f * row[1], sps, sgs);
+    sp_sig1(kLogExpm1One + 0.1f * row[ST], sps, sgs);
     const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
     const float zz = (z - row[0]) * rs;
     const float gz = gl * zz * rs;
     a1 = -gz;
     row[0] = gz;
-    row[1] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+    row[ST] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
   } else {
     a1 = -gl * z;
   }
@@ -340,7 +348,7 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
   float pb[3] = {0.0f, 0.0f, 0.0f};
   float zb = 0.0f;
   if (K > 0) {
-    read3c(pb, row, ob);
+    read3c<ST>(pb, row, ob);
     zb = zh[(K - 1) * zs];
   }
 #pragma unroll 1
@@ -349,9 +357,9 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
       const int ip = (int)((types >> (2 * (k - 1) & 31)) & 3u);
       const int op = min(ob + size1(ib), P - 1);  // k = 0: a harmless in-slot read
       float pp[3];
-      read3c(pp, row, op);
+      read3c<ST>(pp, row, op);
       const float zp = zh[max(k - 1, 0) * zs];
-      flow1_bwd(ib, zb, a1, pb, row + ob, gl);
+      flow1_bwd<ST>(ib, zb, a1, pb, row + ob * ST, gl);
       ib = ip;
       ob = op;
       pb[0] = pp[0];

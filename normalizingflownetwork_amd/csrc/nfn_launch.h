@@ -81,6 +81,11 @@ bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_
 // wave's LDS region in floats
 constexpr int kCS = 68;
 __host__ __device__ inline int dense1_wave_floats(int P, int SH) { return std::max(64 * SH, (P + 1) * kCS); }
+// chain_dense1_grad_kernel: the t tile ((P + 2) columns) + K x 64 flow inputs, the h
+// rows (64 x SH) overlaying both (dead before either is written)
+__host__ __device__ inline int dense1_grad_wave_floats(int P, int SH, int K) {
+  return std::max(64 * SH, (P + 2) * kCS + K * 64);
+}
 // nfn_dense.hip; false if (dm, H) has no instance
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_posterior_dense(bool fast, int dm, const DenseArgs& da, hipStream_t s, int64_t* grid);

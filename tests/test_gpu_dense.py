@@ -229,3 +229,52 @@ def test_dense_grad_fallback_and_full_size(gpu):
     _, gh12, gW12, gb12, _ = ops.chain_log_prob_dense_grad(y[:300], h12, W12, b, ft, d, True)
     _, gt12, _ = ops.chain_log_prob_grad(y[:300], h12 @ W12 + b, ft, d, True)
     torch.testing.assert_close(gW12, h12.t() @ gt12)
+
+
+@pytest.mark.parametrize("ft,H,B,trainable,g_none", [
+    (("planar", "radial") * 5, 16, 64 * 37 + 5, True, False),
+    (("affine", "planar", "radial", "affine"), 16, 640, False, True),
+    (("radial", "planar") * 3 + ("affine",), 32, 64 * 9 + 63, True, True),
+    (("planar",) * 16, 32, 77, False, False),
+    (("radial",), 16, 1, True, False)])
+def test_dense1_grad_kernel_shapes(gpu, ft, H, B, trainable, g_none):
+    """The d = 1 fast-math fused Dense backward (chain_dense1_grad_kernel: H in {16, 32},
+    P <= 64) over ragged batches, widths P not a multiple of 16, a fixed base, a missing
+    upstream gradient (= ones) and y normalisation (mean 0.25, std 2: the kernel's
+    (y - m) / s is then bitwise numpy's), against the autodiff oracle as above."""
+    from oracle import nfn_grad_oracle as G
+    from normalizingflownetwork_amd import ops
+
+    d = 1
+    rng = np.random.default_rng(B + H)
+    P = O.total_param_size(ft, d, trainable)
+    h = rng.standard_normal((B, H)).astype(np.float32)
+    W = (rng.standard_normal((H, P)) / np.sqrt(H)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(P)).astype(np.float32)
+    y = rng.standard_normal((B, d)).astype(np.float32)
+    t32 = (h @ W + b).astype(np.float32)
+    g = None if g_none else rng.standard_normal(B).astype(np.float32)
+    ym, ys = np.float32(0.25), np.float32(2.0)
+    z = ((y - ym) / ys).astype(np.float32)
+    lp, gh, gW, gb, gy = ops.chain_log_prob_dense_grad(
+        torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(), torch.from_numpy(W).cuda(), torch.from_numpy(b).cuda(),
+        ft, d, trainable, y_mean=torch.tensor([ym]).cuda(), y_std=torch.tensor([ys]).cuda(),
+        g_out=None if g is None else torch.from_numpy(g).cuda(), want_logp=True)
+    gg = np.ones(B, np.float32) if g is None else g
+    gt64, gy64, dev_t, dev_y = G.fp32_spread(z, t32, ft, d, trainable, g_out=gg)
+    bt = G.grad_tolerance(gt64, dev_t)
+    assert np.isfinite(gt64).all()
+    W64, h64 = W.astype(np.float64), h.astype(np.float64)
+    gh_ref, gW_ref, gb_ref = gt64 @ W64.T, h64.T @ gt64, gt64.sum(0)
+    bh = bt @ np.abs(W64).T + 1e-5 * (np.abs(gt64) @ np.abs(W64).T) + 1e-7
+    bW = np.abs(h64).T @ bt + 1e-5 * (np.abs(h64).T @ np.abs(gt64)) + 1e-6
+    bb = bt.sum(0) + 1e-5 * np.abs(gt64).sum(0) + 1e-6
+    for got, ref, bound, what in ((gh, gh_ref, bh, "dh"), (gW, gW_ref, bW, "dW"), (gb, gb_ref, bb, "db")):
+        err = np.abs(got.cpu().numpy().astype(np.float64) - ref)
+        assert (err <= bound).all(), f"{what}: max err/bound {np.max(err / bound):.3g}"
+    ey = np.abs(gy.cpu().numpy() - gy64 / 2.0)
+    assert (ey <= G.grad_tolerance(gy64 / 2.0, dev_y / 2.0)).all(), "dy"
+    t64 = h64 @ W64 + b.astype(np.float64)
+    ref64 = O.chain_log_prob(z, t64, ft, d, trainable, np.float64) - np.log(2.0)
+    ref32 = O.chain_log_prob(z, t32, ft, d, trainable, np.float32) - np.float32(np.log(2.0))
+    assert np.all(np.abs(lp.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32))

@@ -84,7 +84,9 @@ for s in $STEPS; do
     valu) run valu 300 python tools/microbench.py valu ;;
     c3micro) run c3micro 300 python tools/microbench.py c3 ;;
     dense) run bench_dense 300 python bench.py --mode dense --steps 50 --warmup 10 --cpu-seconds 6 ;;
-    densetests) run densetests 300 python -m pytest tests/test_gpu_dense.py -m gpu -q -p no:cacheprovider ;;
+    densetests) run densetests 300 python -u -m pytest tests/test_gpu_dense.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    gradtests) run gradtests 300 python -u -m pytest tests/test_gpu_grad.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    dgradmicro) run dgradmicro 300 python tools/microbench.py dgrad ;;
     prof_grad_c3)
       { cd /tmp; run rocprof_grad_c3 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_grad_c3" -o gradc3 -- \
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 20 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
@@ -105,6 +107,11 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write_grad_c3 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_grad_c3" -o w -- \
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_sq_dgrad)  # stall breakdown of the fused Dense backward (two counter passes)
+      { cd /tmp; run pmc_sq1_dgrad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_sq1_dgrad" -o s1 -- \
+        python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_sq2_dgrad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_sq2_dgrad" -o s2 -- \
+        python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;

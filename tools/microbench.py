@@ -233,16 +233,30 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
         _, gt, gy = ops.chain_log_prob_grad(y, tt, ft, d, True, g_out=g)
         return gt @ W.t(), h.t() @ gt, gt.sum(0), gy
 
+    fused = lambda: ops.chain_log_prob_dense_grad(y, h, W, b, ft, d, True, g_out=g)
     fns = {
-        "fused": lambda: ops.chain_log_prob_dense_grad(y, h, W, b, ft, d, True, g_out=g),
+        "fused": fused,
+        "fused_generic": fused,
+        "fused_gemms_only": fused,
         "unfused": unfused,
         "chain_backward_on_resident_t": lambda: ops.chain_log_prob_grad(y, t, ft, d, True, g_out=g),
     }
+    envs = {"fused_generic": {"NFN_DENSE1_GRAD": "0"}, "fused_gemms_only": {"NFN_ABLATE_FLOWS": "1"}}
+    ref = [x for x in fused()[1:]]
+    os.environ["NFN_DENSE1_GRAD"] = "0"
+    gen_out = [x for x in fused()[1:]]
+    del os.environ["NFN_DENSE1_GRAD"]
+    for name, a_, b_ in zip(("dh", "dW", "db", "dy"), ref, gen_out):
+        print(json.dumps({"check": "dense1_grad vs generic", "what": name,
+                          "max_rel": float(((a_ - b_).abs() / (b_.abs() + 1e-30)).max().item()),
+                          "max_abs": float((a_ - b_).abs().max().item())}), flush=True)
     stream = torch.cuda.current_stream()
     prewarm(fns["fused"])
     times = {k: [] for k in fns}
     for r in range(rounds):
         for k, fn in fns.items():
+            saved = {e: os.environ.get(e) for e in envs.get(k, {})}
+            os.environ.update(envs.get(k, {}))
             for _ in range(3):
                 fn()
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -252,6 +266,11 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
                 e1.record(stream)
             torch.cuda.synchronize()
             times[k].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+            for e, v in saved.items():
+                if v is None:
+                    os.environ.pop(e, None)
+                else:
+                    os.environ[e] = v
     for k in fns:
         ms = float(np.median(times[k]))
         print(json.dumps({"cfg": "C2", "mode": "dense_grad", "H": H, "B": B, "variant": k, "ms": ms,
