@@ -14,7 +14,7 @@ all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
 resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
-                  [--mode forward|grad|dense|dense_grad]
+                  [--mode forward|grad|dense|dense_grad|bijector]
   N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
   bench.py --gpus N), or plain `python bench.py --gpus N`, which starts that launcher as a
   child process itself (before touching the GPU) and exits with its status.
@@ -99,6 +99,18 @@ def _cpu_job(kind: str, cfg: str, rows: int, seed: int, H: int):
             return (lambda: O.chain_log_prob(y, t, ft, d, True, np.float32)), rows
         t = rng.standard_normal((S, rows, P)).astype(np.float32)
         return (lambda: O.posterior_lse(y, t, ft, d, True, dtype=np.float32)), rows * S
+    if kind == "bijector":
+        t = rng.standard_normal((rows, P)).astype(np.float32)
+        _, blocks = O.split_params(t, ft, d, True)
+
+        def chain():
+            z, ldj = y, np.zeros(rows, np.float32)
+            for f, tk in zip(ft, blocks):
+                z, l = O.flow_forward_fldj(f, z, tk, d)
+                ldj = ldj + l
+            return z, ldj
+
+        return chain, rows
     if kind == "grad":
         from oracle import nfn_grad_oracle as G
 
@@ -157,7 +169,7 @@ def cpu_baseline(kind: str, cfg: str, H: int = 16, seconds: float = 8.0) -> dict
     import multiprocessing as mp
 
     ft, d, _, S = CONFIGS[cfg]
-    total = {"forward": 1 << 20, "dense": 1 << 20, "grad": 1 << 16, "dense_grad": 1 << 16}[kind]
+    total = {"forward": 1 << 20, "dense": 1 << 20, "grad": 1 << 16, "dense_grad": 1 << 16, "bijector": 1 << 20}[kind]
     if S is not None:
         total = max(64, total // S)
     n = cpu_workers()
@@ -176,6 +188,7 @@ def cpu_baseline(kind: str, cfg: str, H: int = 16, seconds: float = 8.0) -> dict
     unit_rows = "(draw, sample) pairs" if S is not None else "samples"
     what = {"forward": "numpy fp32 op-by-op chain", "dense": "numpy fp32 GEMM + op-by-op chain",
             "grad": "torch fp32 autodiff of the eager op sequence",
+            "bijector": "numpy fp32 flow-by-flow forward + fldj",
             "dense_grad": "numpy GEMM + torch fp32 autodiff of the eager op sequence + weight-gradient GEMMs"}[kind]
     return {
         "value": pooled,
@@ -251,11 +264,13 @@ def main():
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
-    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad", "bijector"],
                     help="forward = fused log_prob (the headline); grad = the fused backward of the "
                          "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient); dense = the "
                          "output Dense layer (H -> P) fused into the chain, streaming h instead of t; "
-                         "dense_grad = the training step's backward through that fused layer (dh, dW, db, dy)")
+                         "dense_grad = the training step's backward through that fused layer (dh, dW, db, dy); "
+                         "bijector = the Bijector API's Chain.forward + forward_log_det_jacobian over the "
+                         "layer's flows in one launch (no base density)")
     ap.add_argument("--hidden", type=int, default=16, help="--mode dense / dense_grad: hidden width H")
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the all-reduce even at N = 1 (tests)")
@@ -304,6 +319,10 @@ def main():
             launcher = ops.DenseGradLauncher(y, h, Wd, bd, ft, d, True, g_out=g_up)
         else:
             launcher = (ops.DenseLauncher if S is None else ops.PosteriorDenseLauncher)(y, h, Wd, bd, ft, d, True)
+    elif args.mode == "bijector":
+        assert S is None, "--mode bijector covers the plain chain configs (C2, C3)"
+        t = torch.randn((B, P), generator=gen, device=dev)
+        launcher = ops.BijectorLauncher(y, t, ft, d, True)
     else:
         t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
         if grad_mode:
@@ -333,7 +352,7 @@ def main():
         launcher.launch(sh)
         if ev1 is not None:
             ev1.record(stream)
-        if grad_mode:  # per-sample gradients stay on their rank (the MLP's would be all-reduced)
+        if grad_mode or args.mode == "bijector":  # per-sample outputs stay on their rank
             return
         s = launcher.finish_sum(sh)
         if native is not None:
@@ -434,7 +453,19 @@ def main():
             plain.launch(sh)
             gt = plain.grad_t
             return gt @ Wd.t(), h.t() @ gt, gt.sum(0)
-    if dense_mode and rank == 0:
+    elif args.mode == "bijector" and rank == 0:
+        # the same Chain through the flow-by-flow Bijector path (one single-flow launch per
+        # flow: each reads its block's cache lines of t again)
+        from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+        from normalizingflownetwork_amd.normalizing_flows import Chain
+
+        flows = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d).bijectors
+        steps = Chain([type(f)(f.params, d) for f in flows])
+        steps._fused = lambda: None
+
+        def unfused():
+            steps.forward_and_log_det_jacobian(y)
+    if (dense_mode or args.mode == "bijector") and rank == 0:
         for _ in range(3):
             unfused()
         pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
@@ -444,9 +475,10 @@ def main():
             e1.record(stream)
         torch.cuda.synchronize()
         unfused_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in pairs]))
-        del t_buf, plain
+        if dense_mode:
+            del t_buf, plain
     nonfinite = None
-    if grad_mode:
+    if grad_mode or args.mode == "bijector":
         mean_ll = None
     elif native is not None:
         mean_ll = float(native.mean.item())
@@ -467,14 +499,17 @@ def main():
         elif args.mode == "dense":
             nd = 1 if S is None else S
             bytes_launch = float(B) * (4 * H * nd + 4 * d + 4) + nd * (4.0 * H * P + 4.0 * P)
+        elif args.mode == "bijector":
+            # z in, the flows' blocks of t (P - 2d floats), z_K and ldj out
+            bytes_launch = float(B) * (4 * d + 4 * (P - 2 * d) + 4 * d + 4)
         elif args.mode == "dense_grad":
             # h, y, upstream g in; dh, dy out; W, b read and dW, db written once per launch
             bytes_launch = float(B) * (8 * H + 8 * d + 4) + 2 * (4.0 * H * P + 4.0 * P)
         else:
             bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense",
-                                                           "dense_grad": "_dense_grad"}.get(args.mode, ""), B)
+        traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense", "dense_grad": "_dense_grad",
+                                                           "bijector": "_bijector"}.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.mode, args.config, H=H, seconds=args.cpu_seconds)
@@ -490,6 +525,9 @@ def main():
             kernel_name = ("chain_dense1_grad_kernel" if d == 1 and H in (16, 32) else "chain_dense_grad_kernel") + \
                 " + sum_partials_kernel"
             metric = f"Dense(H={H})->log_prob backward evals/sec (whole node), {args.config}"
+        elif args.mode == "bijector":
+            kernel_name = "chain_wave1_kernel (Chain bijector form)" if d == 1 else "chain_fwd_ldj_kernel"
+            metric = f"Chain bijector forward+fldj evals/sec (whole node), {args.config}"
         elif args.mode == "dense":
             if S is None:
                 kernel_name = "chain_dense1_kernel" if d == 1 else "chain_dense_kernel"

@@ -53,6 +53,9 @@
  *                             RadialFlow._forward/_forward_log_det_jacobian
  *                                                    estimators/normalizing_flows/RadialFlow.py:20-84
  *                             AffineFlow (tfp Affine) estimators/normalizing_flows/AffineFlow.py:4-9
+ *   nfn_chain_fwd_ldj_f32  <- tfp Chain(flows).forward / .forward_log_det_jacobian as composed by
+ *                             InverseNormalizingFlowLayer._get_bijector
+ *                                                    estimators/DistributionLayers.py:267-278
  *   nfn_posterior_lse_f32  <- BayesianNNEstimator.score per-sample logsumexp
  *                                                    estimators/BayesianNNEstimator.py:65-76,
  *                                                    evaluation/scorers.py:13-27
@@ -204,6 +207,19 @@ int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32
 int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
                              int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out,
                              void* stream);
+
+/*
+ * The Bijector API's Chain of flows in ONE launch (instead of one launch per flow):
+ *   z_out[b]   = f_{K-1}( ... f_0(z[b]) )       (flow_ids in APPLICATION order, f_0 first)
+ *   ldj_out[b] = sum_k log|det J_k|             (summed in application order, as tfp Chain)
+ *   t : (B, >= span) rows at t_rowstride floats (0 = one row broadcast); flow k reads its
+ *       param_size(flow_ids[k], d) floats at t + b*t_rowstride + block_offsets[k]
+ *       (e.g. the layer's reversed layout: the views a Chain's flows hold into one t)
+ *   z_out : (B, d) contiguous, may be NULL; ldj_out : (B,), may be NULL
+ */
+int32_t nfn_chain_fwd_ldj_f32(const float* z, int64_t z_bstride, const float* t, int64_t t_rowstride, int64_t B,
+                              int32_t d, const int32_t* flow_ids, const int32_t* block_offsets, int32_t K,
+                              float* z_out, float* ldj_out, void* stream);
 
 /* out[0] = sum of the n doubles at `in` (device), one workgroup, fixed order
  * (deterministic). */

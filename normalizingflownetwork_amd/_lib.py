@@ -37,6 +37,10 @@ SIGNATURES = {
         _c_int32,
         [_c_int32, _vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _vp, _vp],
     ),
+    "nfn_chain_fwd_ldj_f32": (
+        _c_int32,
+        [_vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _vp, _c_int32, _vp, _vp, _vp],
+    ),
     "nfn_posterior_lse_f32": (
         _c_int32,
         [

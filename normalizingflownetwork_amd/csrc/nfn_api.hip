@@ -829,4 +829,89 @@ int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride,
   return check_hip("flow_fwd_ldj_kernel launch");
 }
 
+int32_t nfn_chain_fwd_ldj_f32(const float* z, int64_t z_bstride, const float* t, int64_t t_rowstride, int64_t B,
+                              int32_t d, const int32_t* flow_ids, const int32_t* block_offsets, int32_t K,
+                              float* z_out, float* ldj_out, void* stream) {
+  g_last_error.clear();
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
+  if (K < 0 || K > NFN_MAX_FLOWS) return fail(NFN_E_FLOW_ID, "number of flows must be in [0, " + std::to_string(NFN_MAX_FLOWS) + "]");
+  if (K > 0 && (!flow_ids || !block_offsets)) return fail(NFN_E_NULLPTR, "flow_ids or block_offsets is NULL");
+  if (B < 0 || z_bstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
+  if (z_bstride != 0 && z_bstride < d) return fail(NFN_E_SHAPE, "z batch stride < n_dims");
+  ChainArgs a;
+  memset(&a, 0, sizeof(a));
+  int32_t lo = 0, hi = 0;  // the parameter span [lo, hi) of the row that the flows read
+  for (int32_t k = 0; k < K; ++k) {
+    const int32_t ps = param_size(flow_ids[k], d);
+    if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_ids[k]));
+    if (block_offsets[k] < 0) return fail(NFN_E_SHAPE, "negative block offset");
+    lo = k == 0 ? block_offsets[k] : std::min(lo, block_offsets[k]);
+    hi = std::max(hi, block_offsets[k] + ps);
+  }
+  if (t_rowstride != 0 && t_rowstride < hi) return fail(NFN_E_SHAPE, "t row stride < the flows' parameter span");
+  if (B == 0 || (!z_out && !ldj_out)) return NFN_OK;
+  if (!z || (K > 0 && !t)) return fail(NFN_E_NULLPTR, "z or t is NULL");
+  a.prog.K = K;
+  for (int32_t k = 0; k < K; ++k) {
+    a.prog.step[k] = ((block_offsets[k] - lo) << 2) | flow_ids[k];
+    a.prog.types[k >> 4] |= (uint32_t)flow_ids[k] << (2 * (k & 15));
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // d = 1, fast math, the layer's contiguous reversed blocks (flow k ends where flow k-1's
+  // begins, f_0 last): the packed program derives every offset from the row width, so
+  // the kernel streams the 16-byte-aligned rows [lo & ~3, hi) on the wave1 pipeline
+  {
+    bool layer_layout = K >= 1 && K <= 16;
+    int32_t end = hi;
+    for (int32_t k = 0; layer_layout && k < K; ++k) {
+      end -= param_size(flow_ids[k], d);
+      layer_layout = block_offsets[k] == end;
+    }
+    const int32_t lo4 = lo & ~3;
+    const int32_t Pw = hi - lo4;
+    const int32_t Qw = Pw >> 2;
+    const float* tw = t + lo4;
+    if (layer_layout && end == lo && d == 1 && use_fast_math() && (Pw & 3) == 0 && (Qw & (Qw - 1)) == 0 &&
+        Qw >= 2 && Qw <= 16 && t_rowstride != 0 && (t_rowstride & 3) == 0 &&
+        (reinterpret_cast<uintptr_t>(tw) & 15) == 0 && t_rowstride * 256 < ((int64_t)1 << 31) &&
+        z_bstride * 256 < ((int64_t)1 << 31) && env_int("NFN_WAVE1", 1) != 0) {
+      a.y = z;
+      a.y_bstride = z_bstride;
+      a.t = tw;
+      a.t_rowstride = t_rowstride;
+      a.B = B;
+      a.d = 1;
+      a.P = Pw;
+      a.lds_stride = Pw | 1;
+      a.ntiles = (B + 63) / 64;
+      a.out = ldj_out;
+      a.z_out = z_out;
+      a.nt = 1;
+      a.prio = 1;
+      int64_t grid = 0;
+      if (launch_fwd_ldj_wave1(Qw, a, (size_t)kMaxBlock * a.lds_stride * sizeof(float), s, &grid))
+        return check_hip("chain_wave1_kernel (Chain bijector) launch");
+    }
+  }
+  const int32_t P = hi - lo;
+  const TileGeom g = tile_geom(P);
+  if ((size_t)g.rows * ((size_t)g.lds_stride * sizeof(float)) > (size_t)kLdsMaxBytes)
+    return fail(NFN_E_SHAPE, "parameter span too wide for LDS");
+  a.y = z;
+  a.y_bstride = z_bstride;
+  a.t = K > 0 ? t + lo : t;
+  a.t_rowstride = t_rowstride;
+  a.B = B;
+  a.d = d;
+  a.P = P;
+  a.lds_stride = g.lds_stride;
+  a.tile_rows = g.rows;
+  a.vec4 = (P % 4 == 0 && t_rowstride % 4 == 0 && (reinterpret_cast<uintptr_t>(a.t) & 15) == 0) ? 1 : 0;
+  const int64_t nblk = (B + g.rows - 1) / g.rows;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  launch_chain_fwd_ldj(use_fast_math(), dm_for(d), a, dim3((unsigned)nblk), dim3((unsigned)g.threads), g.lds_bytes,
+                       z_out, ldj_out, s);
+  return check_hip("chain_fwd_ldj_kernel launch");
+}
+
 }  // extern "C"

@@ -99,6 +99,7 @@ struct ChainArgs {
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
+  float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   FlowProgram prog;
 };
 
@@ -1028,7 +1029,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <bool FAST, int Q, bool PACKED>
+// FWD: the Bijector API's Chain forward + forward_log_det_jacobian instead of log_prob
+// (nfn_chain_fwd_ldj_f32 over the layer's flow blocks; needs FAST and PACKED): z_K goes to
+// a.z_out and sum_k log|det J_k| to a.out; no base density, no partial sums.
+template <bool FAST, int Q, bool PACKED, bool FWD = false>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
@@ -1081,10 +1085,12 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   // The previous tile's log_prob, stored through a descriptor bounded at B (empty
   // before the first tile: the store is always issued).  It is issued right AFTER
   // the next prefetch, so the next hand-off's wait (vmcnt(1)) does not cover it.
-  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
-  float pend_v = 0.0f;
+  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0), pend_rz = tile_rsrc(a.z_out, 0);
+  float pend_v = 0.0f, pend_z = 0.0f;
   auto flush = [&]() {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+    if constexpr (FWD)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_z), pend_rz, lane * 4, 0, kNT);
   };
   issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
@@ -1106,13 +1112,19 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     flush();
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     float lp;
-    if constexpr (FAST) {
+    if constexpr (FWD) {
+      static_assert(FAST && PACKED, "the Chain bijector form uses the packed fast-math chain");
+      float z = z0;
+      lp = (a.prog.K > 0 ? chain1_fast_packed(z, tl + lane * S, a.prog.types[0], a.prog.K, a.P) : 0.0f) * kLn2;
+      pend_z = z;
+      pend_rz = tile_rsrc(a.z_out && nr > 0 ? a.z_out + b0 : a.z_out, a.z_out ? nr * 4 : 0);
+    } else if constexpr (FAST) {
       lp = eval_chain1_fast<PACKED>(z0, tl + lane * S, a) - corr;
     } else {
       float z[1] = {z0};
       lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
     }
-    if (lane < nr) {
+    if (!FWD && lane < nr) {
       acc += (double)lp;
       nfc += nonfinite1(lp);
     }

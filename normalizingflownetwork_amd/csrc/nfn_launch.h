@@ -58,6 +58,9 @@ bool launch_persistent_precise(bool post, int dm, int Q, const ChainArgs& a, int
 // nfn_persistent.hip (fast-math unit): d = 1 posterior on the wave1 pipeline, Q in {2, 4, 8, 16}
 void launch_posterior_wave1(int Q, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid);
 int posterior_wave1_wgs_per_cu();
+// nfn_persistent.hip (fast-math unit): the Chain bijector (forward + fldj) on the wave1
+// pipeline for the layer's contiguous reversed blocks, Q in {2, 4, 8, 16}
+bool launch_fwd_ldj_wave1(int Q, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid);
 // nfn_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance
 bool launch_group_fast(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
                        int64_t* grid);
@@ -65,6 +68,8 @@ bool launch_group_precise(bool post, int G, int DPL, int nv, const ChainArgs& a,
                           int64_t* grid);
 // nfn_tile.hip
 void launch_tile(bool fast, bool post, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s);
+void launch_chain_fwd_ldj(bool fast, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, float* z_out,
+                          float* ldj_out, hipStream_t s);
 void launch_flow(bool fast, int dm, int32_t flow_id, const float* z, int64_t z_bstride, const float* tk,
                  int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, hipStream_t s);
 // nfn_grad.hip

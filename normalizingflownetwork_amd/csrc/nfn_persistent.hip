@@ -32,6 +32,18 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }
 
+#if NFN_FAST
+// the Bijector API's Chain (forward + fldj) on the same pipeline (chain_wave1_kernel<FWD>)
+template <int Q>
+void launch_fw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = chain_wave1_kernel<true, Q, true, true>;
+  const int teams = kMaxBlock / 64;
+  const int64_t grid = std::min<int64_t>((a.ntiles + teams - 1) / teams, (int64_t)cu_count() * (a.prog.K >= 4 ? 2 : 4));
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, a);
+}
+#endif
+
 template <bool POST>
 bool try_wave1(int Q, const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* g) {
   // the posterior (C5) stays on the generic kernel: measured 0.177 vs 0.181 ms there
@@ -104,6 +116,16 @@ void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out
 int posterior_wave1_wgs_per_cu() {
   const int w = env_int("NFN_WG_PER_CU", 0);
   return w > 0 ? w : 2;
+}
+
+bool launch_fwd_ldj_wave1(int Q, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid) {
+  switch (Q) {
+    case 2: launch_fw1<2>(a, lds, s, grid); return true;
+    case 4: launch_fw1<4>(a, lds, s, grid); return true;
+    case 8: launch_fw1<8>(a, lds, s, grid); return true;
+    case 16: launch_fw1<16>(a, lds, s, grid); return true;
+  }
+  return false;
 }
 
 void launch_posterior_wave1(int Q, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid) {

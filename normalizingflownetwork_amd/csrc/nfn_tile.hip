@@ -5,6 +5,61 @@
 namespace nfn {
 namespace {
 
+// The Bijector API's Chain (tfp Chain of the flows that InverseNormalizingFlowLayer.
+// _get_bijector builds, DistributionLayers.py:267-278): forward and
+// forward_log_det_jacobian in ONE launch instead of one or two per flow.  A tile of
+// parameter-row spans is staged in LDS (coalesced, odd stride), then every lane applies
+// the flows in application order (the program's block offsets are relative to the
+// span) and writes z_K and sum_k log|det J_k| (summed in application order, as TFP's
+// Chain does).  `a.y` / `a.y_bstride` carry the input z.
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock) chain_fwd_ldj_kernel(ChainArgs a, float* __restrict__ z_out,
+                                                                  float* __restrict__ ldj_out) {
+  extern __shared__ float lds[];
+  const int rows = a.tile_rows > 0 ? a.tile_rows : blockDim.x;
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * rows;
+  const int nr = (int)min((int64_t)rows, a.B - b0);
+  const bool tb = a.t_rowstride == 0;
+  if (a.P > 0) {
+    stage_rows(lds, a.t + (tb ? 0 : b0 * a.t_rowstride), a.t_rowstride, tb ? 1 : nr, a.P, a.lds_stride,
+               a.vec4 != 0);
+  }
+  __syncthreads();
+  if (tid >= nr) return;
+  const int64_t b = b0 + tid;
+  const int d = a.d;
+  float z[DM];
+  const float* zr = a.y + b * a.y_bstride;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) z[j] = j < d ? zr[j] : 0.0f;
+  const float* row = lds + (tb ? 0 : tid * a.lds_stride);
+  float ldj = 0.0f;
+  for (int k = 0; k < a.prog.K; ++k) {
+    const int st = a.prog.step[k];  // wave-uniform (kernel argument)
+    ldj = ldj + flow_step<DM, FAST>(st & 3, z, row + (st >> 2), d);
+  }
+  if (z_out) {
+#pragma unroll
+    for (int j = 0; j < DM; ++j)
+      if (j < d) z_out[b * d + j] = z[j];
+  }
+  if (ldj_out) ldj_out[b] = ldj;
+}
+
+template <bool FAST>
+void launch_c_dm(int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, float* z_out, float* ldj_out,
+                 hipStream_t s) {
+  switch (dm) {
+    case 1: hipLaunchKernelGGL((chain_fwd_ldj_kernel<1, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 2: hipLaunchKernelGGL((chain_fwd_ldj_kernel<2, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 4: hipLaunchKernelGGL((chain_fwd_ldj_kernel<4, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 8: hipLaunchKernelGGL((chain_fwd_ldj_kernel<8, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 16: hipLaunchKernelGGL((chain_fwd_ldj_kernel<16, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    default: hipLaunchKernelGGL((chain_fwd_ldj_kernel<32, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+  }
+}
+
 template <int DM, bool FAST>
 void launch_t(const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool posterior) {
   if (posterior)
@@ -53,6 +108,14 @@ void launch_tile(bool fast, bool post, int dm, const ChainArgs& a, dim3 grid, di
     launch_t_dm<true>(dm, a, grid, block, lds, s, post);
   else
     launch_t_dm<false>(dm, a, grid, block, lds, s, post);
+}
+
+void launch_chain_fwd_ldj(bool fast, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, float* z_out,
+                          float* ldj_out, hipStream_t s) {
+  if (fast)
+    launch_c_dm<true>(dm, a, grid, block, lds, z_out, ldj_out, s);
+  else
+    launch_c_dm<false>(dm, a, grid, block, lds, z_out, ldj_out, s);
 }
 
 void launch_flow(bool fast, int dm, int32_t flow_id, const float* z, int64_t z_bstride, const float* tk,

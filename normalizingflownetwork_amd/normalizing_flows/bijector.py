@@ -111,21 +111,71 @@ class Chain(Bijector):
     def bijectors(self) -> List[Bijector]:
         return self._bijectors
 
+    def _fused(self):
+        """(flow_types in application order, base tensor, column offsets) when every
+        bijector is one of the conditioned flows and their parameter blocks are column
+        views of ONE device tensor (as InverseNormalizingFlowLayer._get_bijector slices
+        t): the whole chain then runs as one kernel launch.  None otherwise."""
+        from .. import ops
+
+        flows = list(reversed(self._bijectors))  # application order
+        if not flows or not all(hasattr(b, "flow_type") and hasattr(b, "params") for b in flows):
+            return None
+        if len({b.n_dims for b in flows}) != 1:
+            return None
+        ps = [b.params for b in flows]
+        p0 = ps[0]
+        if any(p.dim() != 2 or p.stride(1) != 1 or p.dtype != torch.float32 or p.device != p0.device
+               or p.untyped_storage().data_ptr() != p0.untyped_storage().data_ptr()
+               or p.shape[0] != p0.shape[0] or (p.shape[0] > 1 and p.stride(0) != p0.stride(0)) for p in ps):
+            return None
+        base = min(p.data_ptr() for p in ps)
+        offs = [(p.data_ptr() - base) // 4 for p in ps]
+        if any((p.data_ptr() - base) % 4 for p in ps):
+            return None
+        # the base view: same rows, columns from the leftmost block on
+        first = ps[offs.index(0)]
+        width = max(o + p.shape[1] for o, p in zip(offs, ps))
+        if p0.shape[0] > 1 and width > p0.stride(0):
+            return None
+        t = first.as_strided((first.shape[0], width), (first.stride(0) if first.shape[0] > 1 else width, 1))
+        return [b.flow_type for b in flows], t, offs, flows[0].n_dims, ops
+
+    def forward_and_log_det_jacobian(self, x):
+        """``(forward(x), forward_log_det_jacobian(x))``: one kernel launch for a chain of
+        the conditioned flows (``nfn_chain_fwd_ldj_f32``), else one launch per flow."""
+        fz = self._fused()
+        if fz is not None:
+            ft, t, offs, d, ops = fz
+            return ops.chain_forward_ldj(ft, x, t, offs, d)
+        fldj = None
+        for b in reversed(self._bijectors):
+            if hasattr(b, "forward_and_log_det_jacobian"):
+                x, ld = b.forward_and_log_det_jacobian(x)
+            else:
+                ld = b.forward_log_det_jacobian(x, event_ndims=self.forward_min_event_ndims)
+                x = b.forward(x)
+            fldj = ld if fldj is None else fldj + ld
+        if fldj is None:
+            x = torch.as_tensor(x)
+            fldj = torch.zeros(x.shape[:-1], dtype=torch.float32, device=x.device)
+        return x, fldj
+
     def _forward(self, x):
+        fz = self._fused()
+        if fz is not None:
+            ft, t, offs, d, ops = fz
+            return ops.chain_forward_ldj(ft, x, t, offs, d, want_ldj=False)[0]
         for b in reversed(self._bijectors):
             x = b.forward(x)
         return x
 
     def _forward_log_det_jacobian(self, x):
-        fldj = None
-        for b in reversed(self._bijectors):
-            ld = b.forward_log_det_jacobian(x, event_ndims=self.forward_min_event_ndims)
-            fldj = ld if fldj is None else fldj + ld
-            x = b.forward(x)
-        if fldj is None:
-            x = torch.as_tensor(x)
-            return torch.zeros(x.shape[:-1], dtype=torch.float32, device=x.device)
-        return fldj
+        fz = self._fused()
+        if fz is not None:
+            ft, t, offs, d, ops = fz
+            return ops.chain_forward_ldj(ft, x, t, offs, d, want_z=False)[1]
+        return self.forward_and_log_det_jacobian(x)[1]
 
     def _inverse(self, y):
         for b in self._bijectors:

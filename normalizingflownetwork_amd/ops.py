@@ -617,6 +617,33 @@ def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, w
     return z_out, ldj
 
 
+def chain_forward_ldj(flow_types: Sequence[str], z, t, block_offsets: Sequence[int], n_dims: int,
+                      want_z: bool = True, want_ldj: bool = True):
+    """A Chain of flows as ONE kernel launch (``nfn_chain_fwd_ldj_f32``): ``(z_K, sum_k
+    log|det J_k|)`` for flows applied in ``flow_types`` order, flow k reading its block at
+    column ``block_offsets[k]`` of each row of ``t`` (B or 1, >= span).  What tfp's
+    ``Chain.forward`` / ``forward_log_det_jacobian`` compute over the layer's flows
+    (``DistributionLayers.py:267-278``)."""
+    dev = _device()
+    z = _prep_2d(z, n_dims, "z", dev)
+    t = as_device_f32(t, dev)
+    if t.dim() == 1:
+        t = t.unsqueeze(0)
+    assert t.dim() == 2 and (t.shape[0] == 1 or t.stride(1) == 1), "t must be (B, W) with unit column stride"
+    ids, K = flow_ids(flow_types)
+    assert len(block_offsets) == K, "one block offset per flow"
+    offs = (ctypes.c_int32 * max(1, K))(*[int(o) for o in block_offsets])
+    B = max(z.shape[0], t.shape[0])
+    assert z.shape[0] in (1, B) and t.shape[0] in (1, B), "incompatible batch sizes"
+    z_out = torch.empty((B, n_dims), dtype=torch.float32, device=dev) if want_z else None
+    ldj = torch.empty((B,), dtype=torch.float32, device=dev) if want_ldj else None
+    lib = _lib.load()
+    rc = lib.nfn_chain_fwd_ldj_f32(_ptr(z), _row_stride(z), _ptr(t), _row_stride(t), B, int(n_dims), ids, offs, K,
+                                   _ptr(z_out), _ptr(ldj), _stream())
+    _lib.check(rc, "nfn_chain_fwd_ldj_f32")
+    return z_out, ldj
+
+
 def posterior_lse(
     y,
     t_draws,
@@ -667,6 +694,41 @@ def set_math_mode(mode: str) -> str:
     prev = _lib.load().nfn_set_math_mode(1 if mode == "precise" else 0)
     _lib.check(prev if prev < 0 else 0, "nfn_set_math_mode")
     return "precise" if prev == 1 else "fast"
+
+
+class BijectorLauncher:
+    """Pre-bound one-launch Chain bijector (``nfn_chain_fwd_ldj_f32``) over the layer's
+    flow blocks of ``t`` — the Bijector API path (``Chain.forward`` +
+    ``forward_log_det_jacobian``) for the benchmark: ``launch()`` writes ``z_out`` (B, d)
+    and ``ldj`` (B,)."""
+
+    def __init__(self, z: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
+                 trainable_base: bool):
+        self.lib = _lib.load()
+        dev = z.device
+        d = int(n_dims)
+        P = total_param_size(flow_types, d, trainable_base)
+        assert z.dim() == 2 and z.shape[1] == d and z.stride(1) == 1
+        assert t.dim() == 2 and t.shape[1] == P and t.stride(1) == 1
+        self.B = max(int(z.shape[0]), int(t.shape[0]))
+        # the layer's reversed layout: flow k's block offset within the row (_get_bijector)
+        off, offs = 2 * d if trainable_base else 0, [0] * len(flow_types)
+        for k in reversed(range(len(flow_types))):
+            offs[k] = off
+            off += param_size(flow_types[k], d)
+        self.z, self.t = z, t
+        self.z_out = torch.empty((self.B, d), dtype=torch.float32, device=dev)
+        self.ldj = torch.empty((self.B,), dtype=torch.float32, device=dev)
+        self._ids, self._k = flow_ids(flow_types)
+        self._offs = (ctypes.c_int32 * max(1, len(offs)))(*offs)
+        self._args = (_ptr(z), _row_stride(z), _ptr(t), _row_stride(t), self.B, d,
+                      ctypes.cast(self._ids, ctypes.c_void_p), ctypes.cast(self._offs, ctypes.c_void_p), self._k,
+                      _ptr(self.z_out), _ptr(self.ldj))
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self.lib.nfn_chain_fwd_ldj_f32(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_chain_fwd_ldj_f32")
 
 
 class ChainLauncher:

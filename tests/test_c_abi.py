@@ -87,6 +87,16 @@ def test_bad_arguments_are_rejected_before_launch(native_lib):
     # bad flow id in the single-flow entry point
     assert lib.nfn_flow_fwd_ldj_f32(9, fake, 1, fake, 3, 10, 1, fake, fake, None) == -2
     assert lib.nfn_flow_fwd_ldj_f32(0, fake, 1, fake, 2, 10, 1, fake, fake, None) == -1  # stride < 2d+1
+    # the one-launch Chain: unknown flow id, row stride shorter than the blocks' span,
+    # negative offset, NULL offsets; B = 0 is a no-op
+    offs = (ctypes.c_int32 * 2)(3, 0)
+    bad = (ctypes.c_int32 * 2)(0, 9)
+    assert lib.nfn_chain_fwd_ldj_f32(fake, 1, fake, 6, 10, 1, bad, offs, 2, fake, fake, None) == -2
+    assert lib.nfn_chain_fwd_ldj_f32(fake, 1, fake, 5, 10, 1, ids, offs, 2, fake, fake, None) == -1
+    neg = (ctypes.c_int32 * 2)(3, -1)
+    assert lib.nfn_chain_fwd_ldj_f32(fake, 1, fake, 6, 10, 1, ids, neg, 2, fake, fake, None) == -1
+    assert lib.nfn_chain_fwd_ldj_f32(fake, 1, fake, 6, 10, 1, ids, None, 2, fake, fake, None) == -3
+    assert lib.nfn_chain_fwd_ldj_f32(fake, 1, fake, 6, 0, 1, ids, offs, 2, fake, fake, None) == 0
     # posterior with zero draws
     assert lib.nfn_posterior_lse_f32(fake, 1, fake, 80, 8, 0, 10, 1, ids, 2, 1, None, None, fake, None, None,
                                      None) == -1

@@ -389,3 +389,62 @@ def test_radial_tiny_alpha_at_center(d, math_mode):
     lp = lp.cpu().numpy()
     assert np.isfinite(lp).all(), f"{int((~np.isfinite(lp)).sum())} non-finite"
     assert_within(lp, ref64, ref32, f"tiny alpha d={d}")
+
+
+@pytest.mark.parametrize("name,d", [("c2_pr5_d1", 1), ("asym_pra_d3", 3), ("c3_apr_d8", 8), ("planar_radial_d16", 16)])
+def test_chain_bijector_one_launch(name, d, gpu):
+    """The Bijector API's Chain over views of one t runs as ONE launch
+    (nfn_chain_fwd_ldj_f32): bitwise the flow-by-flow path (same per-flow math, ldj summed
+    in application order), and its forward + fldj agree with the fp64 oracle's bijectors
+    (DistributionLayers.py:267-278; PlanarFlow.py / RadialFlow.py / AffineFlow.py)."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer, ops
+    from normalizingflownetwork_amd.normalizing_flows import Chain
+
+    g = load_golden(name)
+    ft, n = g["flow_types"], 777
+    t = torch.as_tensor(g["t"][:n]).cuda()
+    y = torch.as_tensor(g["y"][:n]).cuda()
+    chain = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d)
+    assert chain._fused() is not None
+    launches = []
+    real = ops.chain_forward_ldj
+
+    def counting(*a, **k):
+        launches.append(1)
+        return real(*a, **k)
+
+    ops.chain_forward_ldj = counting
+    try:
+        z, ldj = chain.forward_and_log_det_jacobian(y)
+        assert torch.equal(chain.forward(y), z) and torch.equal(chain.forward_log_det_jacobian(y, event_ndims=1), ldj)
+    finally:
+        ops.chain_forward_ldj = real
+    assert len(launches) == 3
+    # flow by flow through the single-flow kernel (a Chain of copies: no shared storage)
+    steps = Chain([type(b)(b.params.clone(), d) for b in chain.bijectors])
+    assert steps._fused() is None
+    z1, ldj1 = steps.forward_and_log_det_jacobian(y)
+    assert torch.equal(z, z1) and torch.equal(ldj, ldj1)
+    # against the oracle's flows applied in the same order: fp64 truth; the conditioning
+    # term of the bound is the fp32 op-by-op mirror's largest deviation at the inputs and
+    # at three 1-ulp perturbations of them (as O.fp32_spread does for the chain: one fp32
+    # evaluation order can be luckily accurate where the sum over d terms cancels)
+    def oracle(t_, y_, dt):
+        _, blocks = O.split_params(t_.astype(dt), ft, d, True)
+        zr, lr = y_.astype(dt), np.zeros(len(y_), dt)
+        for f, tk in zip(ft, blocks):
+            zr, l = O.flow_forward_fldj(f, zr, tk, d)
+            lr = lr + l
+        return zr.astype(np.float64), lr.astype(np.float64)
+
+    t0, y0 = g["t"][:n], g["y"][:n]
+    z64, l64 = oracle(t0, y0, np.float64)
+    rng = np.random.default_rng(0)
+    dz, dl = np.zeros_like(z64), np.zeros_like(l64)
+    for i in range(4):
+        tp = t0 if i == 0 else (t0 * (1 + rng.choice([-1, 1], t0.shape) * 2.0 ** -23)).astype(np.float32)
+        yp = y0 if i == 0 else (y0 * (1 + rng.choice([-1, 1], y0.shape) * 2.0 ** -23)).astype(np.float32)
+        z32, l32 = oracle(tp, yp, np.float32)
+        dz, dl = np.maximum(dz, np.abs(z32 - z64)), np.maximum(dl, np.abs(l32 - l64))
+    assert (np.abs(ldj.cpu().numpy() - l64) <= np.maximum(1e-5 * np.maximum(1, np.abs(l64)), 8 * dl)).all()
+    assert (np.abs(z.cpu().numpy() - z64) <= np.maximum(1e-5 * np.maximum(1, np.abs(z64)), 8 * dz)).all()

@@ -38,12 +38,25 @@ def test_inverse_then_forward_is_identity(ft, d, gpu):
     # forward chain of the sample in fp64 (the oracle) lands on loc + scale * eps
     base, blocks = O.split_params(t.astype(np.float64), ft, d, True)
     z = y.copy()
+    zs, ls = [np.abs(y).max(1)], []
     for f, tk in zip(ft, blocks):
-        z, _ = O.flow_forward_fldj(f, z, tk, d)
+        z, l = O.flow_forward_fldj(f, z, tk, d)
+        zs.append(np.abs(z).max(1))
+        ls.append(l)
     loc, scale = _base(t, d)
     target = loc + scale * eps
-    err = np.abs(z - target) / np.maximum(1.0, np.abs(target))
-    assert np.quantile(err, 0.999) < 1e-4 and err.max() < 1e-2, (np.quantile(err, 0.999), err.max())
+    # per-sample bound from the inverse walk's own rounding: each step rounds its z_k
+    # once (half an ulp per coordinate), and the forward map from z_k to z_K scales that
+    # by |J_{k->K}| (per coordinate exp(sum_{j>=k} fldj_j / d)); summed over the steps.
+    # Measured (tools/sample_err.py, 2^16 samples per case): max err / bound 2.4-5.5,
+    # 99.9 % quantile <= 1.8 — a step stopped short of convergence lands far above it.
+    tail, gain = np.zeros(B), np.maximum(1.0, zs[-1])
+    for k in range(len(ls) - 1, -1, -1):
+        tail = tail + ls[k]
+        gain = gain + np.exp(tail / d) * np.maximum(1.0, zs[k])
+    err = np.abs(z - target).max(1)
+    bound = 16.0 * 2.0 ** -24 * gain  # 3x the largest measured ratio
+    assert (err <= bound).all(), float((err / bound).max())
     # the sample's log-density is the forward kernel's log_prob of the sample
     lp_fwd, _ = ops.chain_log_prob(torch.from_numpy(y.astype(np.float32)).cuda(), torch.from_numpy(t).cuda(), ft, d,
                                    True)

@@ -183,5 +183,9 @@ def test_fit_fused_dense_matches_unfused(gpu):
         m.fused_dense = fused
         losses[fused] = m.fit(x, y, epochs=50, verbose=0)["loss"]
     assert losses[True][-1] < losses[True][0]
-    np.testing.assert_allclose(losses[True][:10], losses[False][:10], rtol=1e-4)
+    # the first steps agree to fp32 rounding; afterwards the two paths' different GEMM
+    # summation orders (MFMA k-order in the fused kernel vs the library GEMMs) are
+    # amplified by Adam's normalised steps: a few 1e-4 by epoch 10
+    np.testing.assert_allclose(losses[True][:5], losses[False][:5], rtol=1e-5)
+    np.testing.assert_allclose(losses[True][:10], losses[False][:10], rtol=5e-4)
     np.testing.assert_allclose(losses[True][-1], losses[False][-1], rtol=2e-2)

@@ -112,6 +112,9 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_sq2_dgrad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_sq2_dgrad" -o s2 -- \
         python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
+    bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
+    parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    sampleerr) run sampleerr 200 python tools/sample_err.py ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
