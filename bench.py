@@ -173,6 +173,11 @@ def cpu_baseline(kind: str, cfg: str, H: int = 16, seconds: float = 8.0) -> dict
     if S is not None:
         total = max(64, total // S)
     n = cpu_workers()
+    if kind in ("grad", "dense_grad"):
+        # torch's autograd engine initialises the HIP runtime in every worker that runs a
+        # backward (device threads), so those workers hold the GPU open: parent + workers
+        # stay within the 16 processes a leased GPU allows
+        n = min(n, 15)
     one_evals, one_el = _cpu_worker((kind, cfg, total, 22, H, seconds))
     rows = max(64, total // n)
     ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's HIP state is inherited

@@ -115,6 +115,10 @@ for s in $STEPS; do
     bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
     parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     sampleerr) run sampleerr 200 python tools/sample_err.py ;;
+    sampletests) run sampletests 300 python -u -m pytest tests/test_gpu_sample.py tests/test_gpu_training.py -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
+    prof_bij)
+      { cd /tmp; run rocprof_bij 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_bij" -o bij -- \
+        python3 "$ROOT/bench.py" --mode bijector --steps 30 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
