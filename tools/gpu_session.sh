@@ -119,6 +119,16 @@ for s in $STEPS; do
     prof_bij)
       { cd /tmp; run rocprof_bij 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_bij" -o bij -- \
         python3 "$ROOT/bench.py" --mode bijector --steps 30 --warmup 5 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_dgrad)
+      { cd /tmp; run pmc_fetch_dgrad 120 timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_dgrad" -o f -- \
+        python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write_dgrad 120 timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_dgrad" -o w -- \
+        python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_bij)
+      { cd /tmp; run pmc_fetch_bij 120 timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_bij" -o f -- \
+        python3 "$ROOT/bench.py" --mode bijector --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_write_bij 120 timeout -s KILL 100 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_bij" -o w -- \
+        python3 "$ROOT/bench.py" --mode bijector --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
