@@ -338,10 +338,14 @@ def main():
             launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
     stream = torch.cuda.current_stream()
     sh = int(stream.cuda_stream)
-    # (sum, count, non-finite) all-reduce buffers: a ring of two, so step i's all-reduce
+    # (sum, non-finite) all-reduce buffers (the count is B per rank): a ring of two, so step i's all-reduce
     # (async, on the process group's stream) overlaps step i+1's chain kernel; a buffer
-    # is reused only after the stream has waited for its previous all-reduce
-    reds = [torch.zeros((3,), dtype=torch.float64, device=dev) for _ in range(2)]
+    # is reused only after the stream has waited for its previous all-reduce.  Over RCCL
+    # the chain kernel finishes its {sum, non-finite} straight into the ring slot
+    # (ChainLauncher.bind_sum): no copy kernels between the chain and the collective.
+    reds = [torch.zeros((2,), dtype=torch.float64, device=dev) for _ in range(2)]
+    direct = dist_on and args.backend == "nccl" and args.allreduce == "torch" and hasattr(launcher, "bind_sum") \
+        and getattr(launcher, "fused_sum", False)
     works = [None, None]
     nstep = [0]
     evals_per_step = B * (1 if S is None else S)
@@ -352,12 +356,22 @@ def main():
         native = NativeComm()
 
     def step(ev0=None, ev1=None):
+        if direct:
+            i = nstep[0] % 2
+            nstep[0] += 1
+            if works[i] is not None:
+                works[i].wait()  # stream-side wait: the slot's previous all-reduce is done
+            launcher.bind_sum(reds[i])
         if ev0 is not None:
             ev0.record(stream)
         launcher.launch(sh)
         if ev1 is not None:
             ev1.record(stream)
         if grad_mode or args.mode == "bijector":  # per-sample outputs stay on their rank
+            return
+        if direct:
+            works[i] = dist.all_reduce(reds[i], async_op=True)
+            last_red[0] = reds[i]
             return
         s = launcher.finish_sum(sh)
         if native is not None:
@@ -370,13 +384,11 @@ def main():
                 if works[i] is not None:
                     works[i].wait()  # stream-side wait: the buffer's previous all-reduce is done
                 buf[0:1].copy_(s)
-                buf[1] = float(B)
-                buf[2:3].copy_(launcher.nonfinite)
+                buf[1:2].copy_(launcher.nonfinite)
                 works[i] = dist.all_reduce(buf, async_op=True)
             else:  # gloo reduces host tensors
                 buf[0:1].copy_(s)
-                buf[1] = float(B)
-                buf[2:3].copy_(launcher.nonfinite)
+                buf[1:2].copy_(launcher.nonfinite)
                 hb = buf.cpu()
                 dist.all_reduce(hb)
                 buf.copy_(hb)
@@ -490,8 +502,8 @@ def main():
         nonfinite = int(native.sum_count[2].item())
     elif dist_on:
         red = last_red[0]
-        mean_ll = float(red[0].item() / red[1].item())
-        nonfinite = int(red[2].item())
+        mean_ll = float(red[0].item()) / float(B * world)
+        nonfinite = int(red[1].item())
     else:
         mean_ll = float(launcher.sum.item()) / B
         nonfinite = int(launcher.nonfinite.item())

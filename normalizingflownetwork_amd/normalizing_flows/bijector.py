@@ -129,16 +129,20 @@ class Chain(Bijector):
                or p.untyped_storage().data_ptr() != p0.untyped_storage().data_ptr()
                or p.shape[0] != p0.shape[0] or (p.shape[0] > 1 and p.stride(0) != p0.stride(0)) for p in ps):
             return None
+        storage0 = p0.untyped_storage().data_ptr()
         base = min(p.data_ptr() for p in ps)
-        offs = [(p.data_ptr() - base) // 4 for p in ps]
+        # start the view at the 16-byte boundary at or before the leftmost block (within the
+        # storage): the layer's rows then stream as aligned float4 (the base columns to the
+        # left are staged, never read)
+        base = max(storage0, base - base % 16)
         if any((p.data_ptr() - base) % 4 for p in ps):
             return None
-        # the base view: same rows, columns from the leftmost block on
-        first = ps[offs.index(0)]
+        offs = [(p.data_ptr() - base) // 4 for p in ps]
         width = max(o + p.shape[1] for o, p in zip(offs, ps))
-        if p0.shape[0] > 1 and width > p0.stride(0):
+        rs = p0.stride(0) if p0.shape[0] > 1 else width
+        if p0.shape[0] > 1 and width > rs:
             return None
-        t = first.as_strided((first.shape[0], width), (first.stride(0) if first.shape[0] > 1 else width, 1))
+        t = p0.as_strided((p0.shape[0], width), (rs, 1), (base - storage0) // 4)
         return [b.flow_type for b in flows], t, offs, flows[0].n_dims, ops
 
     def forward_and_log_det_jacobian(self, x):

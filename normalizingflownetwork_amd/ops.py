@@ -786,6 +786,16 @@ class ChainLauncher:
         if rc != 0:
             _lib.check(rc, "fused chain launch")
 
+    def bind_sum(self, target: torch.Tensor) -> None:
+        """Make later launches finish their ``{sum, non-finite count}`` into ``target[0:2]``
+        (fp64, device) — e.g. straight into an all-reduce buffer, so a multi-GPU step needs
+        no copy kernels between the chain kernel and the collective."""
+        assert self.fused_sum, "bind_sum needs the in-kernel finish"
+        assert target.dtype == torch.float64 and target.is_contiguous() and target.numel() >= 2
+        i = 14 if self.posterior else 12
+        self._args = self._args[:i] + (_ptr(target),) + self._args[i + 1:]
+        self.sum2, self.sum = target[0:2], target[0:1]
+
     def finish_sum(self, stream: Optional[int] = None) -> torch.Tensor:
         """``sum`` (1,) fp64 of the last launch: finished inside the kernel by default; with
         ``fused_sum=False`` the launch writes only the partials and this reduces them

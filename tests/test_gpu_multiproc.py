@@ -51,7 +51,15 @@ def test_bench_nccl_step_path_one_rank(gpu, allreduce):
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
-    assert out["n_gpus"] == 1 and np.isfinite(out["mean_log_prob"])
+    assert out["n_gpus"] == 1 and out["pg_world_size"] == 1 and np.isfinite(out["mean_log_prob"])
+    # the RCCL step path (the kernel finishing its sum straight into the all-reduce ring for
+    # torch, the library communicator for native) gives exactly the plain N = 1 mean
+    plain = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "2",
+             "--batch", str(1 << 18), "--no-cpu-baseline"]
+    r1 = subprocess.run(plain, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    ref = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][0])
+    assert out["mean_log_prob"] == ref["mean_log_prob"] and out["nonfinite_log_prob"] == ref["nonfinite_log_prob"]
 
 
 def test_bench_spawns_its_ranks(gpu):

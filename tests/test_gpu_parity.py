@@ -405,7 +405,11 @@ def test_chain_bijector_one_launch(name, d, gpu):
     t = torch.as_tensor(g["t"][:n]).cuda()
     y = torch.as_tensor(g["y"][:n]).cuda()
     chain = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d)
-    assert chain._fused() is not None
+    fz = chain._fused()
+    assert fz is not None
+    # the fused view starts at the 16-byte row boundary left of the first block (d = 1: the
+    # base columns), so the layer's rows stream as aligned float4 on the wave1 pipeline
+    assert fz[1].data_ptr() % 16 == 0 and min(fz[2]) == 2 * d % 4 + (2 * d // 4) * 4 - (fz[1].data_ptr() - t.data_ptr()) // 4
     launches = []
     real = ops.chain_forward_ldj
 
