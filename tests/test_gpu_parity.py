@@ -409,7 +409,7 @@ def test_chain_bijector_one_launch(name, d, gpu):
     assert fz is not None
     # the fused view starts at the 16-byte row boundary left of the first block (d = 1: the
     # base columns), so the layer's rows stream as aligned float4 on the wave1 pipeline
-    assert fz[1].data_ptr() % 16 == 0 and min(fz[2]) == 2 * d % 4 + (2 * d // 4) * 4 - (fz[1].data_ptr() - t.data_ptr()) // 4
+    assert fz[1].data_ptr() % 16 == 0 and min(fz[2]) + (fz[1].data_ptr() - t.data_ptr()) // 4 == 2 * d
     launches = []
     real = ops.chain_forward_ldj
 
