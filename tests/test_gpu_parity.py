@@ -424,11 +424,14 @@ def test_chain_bijector_one_launch(name, d, gpu):
     finally:
         ops.chain_forward_ldj = real
     assert len(launches) == 3
-    # flow by flow through the single-flow kernel (a Chain of copies: no shared storage)
+    # flow by flow through the single-flow kernel (a Chain of copies: no shared storage);
+    # bitwise the one-launch result where both run the generic per-flow math (d > 1; d = 1
+    # runs the packed fast-math chain on the wave1 pipeline: both are held to the oracle below)
     steps = Chain([type(b)(b.params.clone(), d) for b in chain.bijectors])
     assert steps._fused() is None
     z1, ldj1 = steps.forward_and_log_det_jacobian(y)
-    assert torch.equal(z, z1) and torch.equal(ldj, ldj1)
+    if d > 1:
+        assert torch.equal(z, z1) and torch.equal(ldj, ldj1)
     # against the oracle's flows applied in the same order: fp64 truth; the conditioning
     # term of the bound is the fp32 op-by-op mirror's largest deviation at the inputs and
     # at three 1-ulp perturbations of them (as O.fp32_spread does for the chain: one fp32
@@ -450,5 +453,6 @@ def test_chain_bijector_one_launch(name, d, gpu):
         yp = y0 if i == 0 else (y0 * (1 + rng.choice([-1, 1], y0.shape) * 2.0 ** -23)).astype(np.float32)
         z32, l32 = oracle(tp, yp, np.float32)
         dz, dl = np.maximum(dz, np.abs(z32 - z64)), np.maximum(dl, np.abs(l32 - l64))
-    assert (np.abs(ldj.cpu().numpy() - l64) <= np.maximum(1e-5 * np.maximum(1, np.abs(l64)), 8 * dl)).all()
-    assert (np.abs(z.cpu().numpy() - z64) <= np.maximum(1e-5 * np.maximum(1, np.abs(z64)), 8 * dz)).all()
+    for zz, ll in ((z, ldj), (z1, ldj1)):
+        assert (np.abs(ll.cpu().numpy() - l64) <= np.maximum(1e-5 * np.maximum(1, np.abs(l64)), 8 * dl)).all()
+        assert (np.abs(zz.cpu().numpy() - z64) <= np.maximum(1e-5 * np.maximum(1, np.abs(z64)), 8 * dz)).all()

@@ -7,6 +7,7 @@ back to back with HIP events on the launch stream.  Outputs are also checked
 against the first variant (max |diff|)."""
 
 import json
+import time
 import os
 import sys
 
@@ -310,8 +311,56 @@ def run_finish(cfgs=("C2", "C5", "C3"), reps=30, rounds=4):
                               "rounds_ms": times[k], "sum_nonfinite": sums[k]}), flush=True)
 
 
+def run_pcie(reps=5):
+    """The drop-in path with HOST inputs (the reference hands numpy arrays to TF on the CPU):
+    C2 log_prob end to end — y, t host -> device, the fused kernel, log_prob device -> host —
+    from pageable numpy arrays (what ops.chain_log_prob(numpy, numpy) does) and from pinned
+    host tensors with async copies; the device-resident kernel alone for comparison."""
+    ft, d, B, _ = CFG["C2"]
+    P = ops.total_param_size(ft, d, True)
+    rng = np.random.default_rng(0)
+    y_np = rng.standard_normal((B, d)).astype(np.float32)
+    t_np = rng.standard_normal((B, P)).astype(np.float32)
+    y_pin, t_pin = torch.from_numpy(y_np).pin_memory(), torch.from_numpy(t_np).pin_memory()
+    out_pin = torch.empty((B,), dtype=torch.float32).pin_memory()
+    yd, td = y_pin.cuda(), t_pin.cuda()
+
+    def pageable():
+        lp, _ = ops.chain_log_prob(y_np, t_np, ft, d, True)
+        return lp.cpu()
+
+    def pinned():
+        yd.copy_(y_pin, non_blocking=True)
+        td.copy_(t_pin, non_blocking=True)
+        lp, _ = ops.chain_log_prob(yd, td, ft, d, True)
+        out_pin.copy_(lp, non_blocking=True)
+        torch.cuda.synchronize()
+        return out_pin
+
+    def resident():
+        lp, _ = ops.chain_log_prob(yd, td, ft, d, True)
+        torch.cuda.synchronize()
+        return lp
+
+    for name, fn in (("host_pageable", pageable), ("host_pinned", pinned), ("device_resident", resident)):
+        fn()
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ms = float(np.median(ts)) * 1e3
+        print(json.dumps({"cfg": "C2", "mode": "pcie", "variant": name, "ms": ms, "evals_per_s": B / ms * 1e3,
+                          "h2d_bytes": B * (d + P) * 4 if name != "device_resident" else 0}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "pcie":
+        run_pcie()
+        return
     if which[0] == "finish":
         run_finish()
         return
