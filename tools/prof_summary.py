@@ -26,6 +26,24 @@ def find(root, pattern):
     return hits
 
 
+def cmd_trace(args):
+    """Per-call durations of one kernel from a kernel_trace.csv: mean / median over all calls
+    and over the last N (the bench's timed steps, after its prewarm and warmup)."""
+    src = find(args.dir, "*kernel_trace.csv")[0]
+    with open(src) as f:
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(f)
+             if r["Kernel_Name"].startswith(args.kernel)]
+    if not d:
+        raise SystemExit(f"no {args.kernel} calls in {src}")
+    last = d[-args.last:]
+    rec = {"kernel": args.kernel, "calls": len(d), "mean_us": statistics.mean(d), "median_us": statistics.median(d),
+           "min_us": min(d), "max_us": max(d), "last_n": len(last), "last_mean_us": statistics.mean(last),
+           "last_median_us": statistics.median(last)}
+    with open(args.out_json, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+
+
 def cmd_stats(args):
     src = find(args.dir, "*kernel_stats.csv")[0]
     shutil.copyfile(src, args.out_prefix + "_kernel_stats.csv")
@@ -88,6 +106,12 @@ def main():
     s = sub.add_parser("stats")
     s.add_argument("dir")
     s.add_argument("out_prefix")
+    tr = sub.add_parser("trace")
+    tr.add_argument("dir")
+    tr.add_argument("out_json")
+    tr.add_argument("--kernel", default="chain_wave1_kernel")
+    tr.add_argument("--last", type=int, default=50)
+    tr.set_defaults(fn=cmd_trace)
     p = sub.add_parser("pmc")
     p.add_argument("fetch_dir")
     p.add_argument("write_dir")
@@ -97,7 +121,7 @@ def main():
     p.add_argument("--kernel", default="chain_logprob")
     p.add_argument("--alg-bytes", type=float, default=None)
     args = ap.parse_args()
-    {"stats": cmd_stats, "pmc": cmd_pmc}[args.cmd](args)
+    {"stats": cmd_stats, "pmc": cmd_pmc, "trace": cmd_trace}[args.cmd](args)
 
 
 if __name__ == "__main__":
