@@ -629,7 +629,7 @@ def chain_forward_ldj(flow_types: Sequence[str], z, t, block_offsets: Sequence[i
     t = as_device_f32(t, dev)
     if t.dim() == 1:
         t = t.unsqueeze(0)
-    assert t.dim() == 2 and (t.shape[0] == 1 or t.stride(1) == 1), "t must be (B, W) with unit column stride"
+    assert t.dim() == 2 and t.stride(1) == 1, "t must be (B, W) with unit column stride"
     ids, K = flow_ids(flow_types)
     assert len(block_offsets) == K, "one block offset per flow"
     offs = (ctypes.c_int32 * max(1, K))(*[int(o) for o in block_offsets])

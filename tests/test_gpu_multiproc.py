@@ -39,15 +39,17 @@ def test_bench_two_ranks_gloo(gpu):
     assert out["mean_log_prob"] == out["mean_log_prob"]
 
 
-@pytest.mark.parametrize("allreduce", ["torch", "native"])
-def test_bench_nccl_step_path_one_rank(gpu, allreduce):
+@pytest.mark.parametrize("allreduce,config", [("torch", "C2"), ("native", "C2"), ("torch", "C5")])
+def test_bench_nccl_step_path_one_rank(gpu, allreduce, config):
     """The N > 1 step path over RCCL (async all-reduce ring / the library's own
-    communicator) exercised with one rank on the one GPU of the test box."""
+    communicator) exercised with one rank on the one GPU of the test box; C5 = the
+    posterior's 8-GPU form (each rank its own 2^17 samples x 64 draws)."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    batch = str(1 << 18) if config == "C2" else str(1 << 14)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "1", "--steps", "5", "--warmup", "2", "--backend", "nccl", "--force-pg",
-           "--allreduce", allreduce, "--batch", str(1 << 18), "--no-cpu-baseline"]
+           "--allreduce", allreduce, "--config", config, "--batch", batch, "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
@@ -55,7 +57,7 @@ def test_bench_nccl_step_path_one_rank(gpu, allreduce):
     # the RCCL step path (the kernel finishing its sum straight into the all-reduce ring for
     # torch, the library communicator for native) gives exactly the plain N = 1 mean
     plain = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "2",
-             "--batch", str(1 << 18), "--no-cpu-baseline"]
+             "--config", config, "--batch", batch, "--no-cpu-baseline"]
     r1 = subprocess.run(plain, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r1.returncode == 0, r1.stderr[-3000:]
     ref = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][0])
