@@ -861,17 +861,51 @@ int32_t nfn_chain_fwd_ldj_f32(const float* z, int64_t z_bstride, const float* t,
   // begins, f_0 last): the packed program derives every offset from the row width, so
   // the kernel streams the 16-byte-aligned rows [lo & ~3, hi) on the wave1 pipeline
   {
-    bool layer_layout = K >= 1 && K <= 16;
+    bool layer_layout = K >= 1;
     int32_t end = hi;
     for (int32_t k = 0; layer_layout && k < K; ++k) {
       end -= param_size(flow_ids[k], d);
       layer_layout = block_offsets[k] == end;
     }
+    layer_layout = layer_layout && end == lo;
+    // d >= 4, fast math, the layer's contiguous rows (the span ends the row and t points at
+    // the row start): the lane-group pipeline of the C3 forward (chain_group1_kernel<FWD>)
+    if (layer_layout && d >= 4 && use_fast_math() && t_rowstride == hi && (hi & 3) == 0 &&
+        (reinterpret_cast<uintptr_t>(t) & 15) == 0 && z_bstride * 256 < ((int64_t)1 << 31) &&
+        env_int("NFN_GROUP1", 1) != 0) {
+      const int dm = dm_for(d);
+      const int Qh = hi >> 2;
+      int G = 4, DPL = 1;
+      group_shape(dm, dm == 8 && (Qh + 1) / 2 <= 18 ? 2 : 0, &G, &DPL);
+      const int R = 64 / G;
+      const int nv = (Qh + G - 1) / G;
+      if (G * DPL >= d && nv <= (G == 2 ? 18 : 16) && (int64_t)R * hi * 4 < ((int64_t)1 << 31)) {
+        a.y = z;
+        a.y_bstride = z_bstride;
+        a.t = t;
+        a.t_rowstride = t_rowstride;
+        a.B = B;
+        a.d = d;
+        a.P = hi;
+        a.lds_stride = group_lds_stride(hi, G);
+        a.ntiles = (B + R - 1) / R;
+        a.out = ldj_out;
+        a.z_out = z_out;
+        a.nt = 1;
+        a.prio = 1;
+        const size_t lds = (size_t)(kMaxBlock / 64) * R * a.lds_stride * sizeof(float) +
+                           std::max<size_t>((G * DPL + 4) * sizeof(float), 64 * 16);
+        int64_t grid = 0;
+        if (launch_group1_fwd(G, DPL, nv, a, lds, s, &grid))
+          return check_hip("chain_group1_kernel (Chain bijector) launch");
+      }
+    }
+    layer_layout = layer_layout && K <= 16;  // the d = 1 packed program holds 16 flows
     const int32_t lo4 = lo & ~3;
     const int32_t Pw = hi - lo4;
     const int32_t Qw = Pw >> 2;
     const float* tw = t + lo4;
-    if (layer_layout && end == lo && d == 1 && use_fast_math() && (Pw & 3) == 0 && (Qw & (Qw - 1)) == 0 &&
+    if (layer_layout && d == 1 && use_fast_math() && (Pw & 3) == 0 && (Qw & (Qw - 1)) == 0 &&
         Qw >= 2 && Qw <= 16 && t_rowstride != 0 && (t_rowstride & 3) == 0 &&
         (reinterpret_cast<uintptr_t>(tw) & 15) == 0 && t_rowstride * 256 < ((int64_t)1 << 31) &&
         z_bstride * 256 < ((int64_t)1 << 31) && env_int("NFN_WAVE1", 1) != 0) {

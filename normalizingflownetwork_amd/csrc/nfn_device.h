@@ -1443,7 +1443,9 @@ __device__ __forceinline__ int flow_type_at(const uint32_t (&tw)[4], int k) {
   return (int)((w >> (2 * (k & 15))) & 3u);
 }
 
-template <int G, int DPL, bool FAST, bool FULL = false>
+// FLOWS_ONLY: the Chain bijector's forward + fldj (no base density): z leaves as z_K and
+// the return value is sum_k log|det J_k| (group-summed, every lane of the group).
+template <int G, int DPL, bool FAST, bool FULL = false, bool FLOWS_ONLY = false>
 __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row, const ChainArgs& a, int j) {
   const int d = FULL ? G * DPL : a.d;
   const int K = a.prog.K;
@@ -1472,6 +1474,7 @@ __device__ __forceinline__ float eval_chain_gd(float (&z)[DPL], const float* row
       }
     }
   }
+  if constexpr (FLOWS_ONLY) return gsum<G>(dimterm) + ildj;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const int jj = j + G * i;
@@ -1633,7 +1636,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
 // tile), y and log_prob by buffer instructions too, and no branch between a load
 // and its use: lanes whose slot lies past the tile write their float4 to a per-lane
 // pad after the last wave slot (distinct addresses: no same-address write conflicts).  Plain chain only (the posterior keeps chain_group_kernel).
-template <int G, int DPL, bool FAST, int NV, bool FULL>
+// FWD: the Bijector API's Chain forward + fldj over the layer's rows (nfn_chain_fwd_ldj_f32):
+// z_K leaves to a.z_out (each lane its DPL dims), sum_k log|det J_k| to a.out; no base density.
+template <int G, int DPL, bool FAST, int NV, bool FULL, bool FWD = false>
 __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
@@ -1711,9 +1716,15 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
     issue(tile + ustep);
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
     if (a.prio) __builtin_amdgcn_s_setprio(0);
-    const float lp = eval_chain_gd<G, DPL, FAST, FULL>(z, tl + sl * S, a, j) - corr;
+    const float lp = eval_chain_gd<G, DPL, FAST, FULL, FWD>(z, tl + sl * S, a, j) - corr;
     wave_lds_sync();  // this tile's LDS reads done before the next writes
-    if (j == 0 && sl < nr) {
+    if constexpr (FWD) {  // z_K: rows past B fall outside the descriptor
+      const auto rz = tile_rsrc(a.z_out && nr > 0 ? a.z_out + b0 * a.d : a.z_out, a.z_out ? (int)nr * a.d * 4 : 0);
+#pragma unroll
+      for (int i = 0; i < DPL; ++i)
+        if (FULL || j + G * i < a.d)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z[i]), rz, (sl * a.d + j + G * i) * 4, 0, kNT);
+    } else if (j == 0 && sl < nr) {
       acc += (double)lp;
       nfc += nonfinite1(lp);
     }

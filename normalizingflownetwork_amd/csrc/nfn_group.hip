@@ -76,9 +76,41 @@ bool launch_g_shape(int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipS
   return false;
 }
 
+#if NFN_FAST
+template <int G, int DPL, int NV>
+void launch_gf(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
+  auto kfn = a.d == G * DPL ? chain_group1_kernel<G, DPL, true, NV, true, true>
+                            : chain_group1_kernel<G, DPL, true, NV, false, true>;
+  int64_t grid = std::min<int64_t>((a.ntiles + 3) / 4, (int64_t)cu_count() * 2);
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, a);
+}
+
+template <int G, int DPL>
+bool launch_gf_nv(int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* g) {
+  if (nv <= 4) launch_gf<G, DPL, 4>(a, lds, s, g);
+  else if (nv <= 8) launch_gf<G, DPL, 8>(a, lds, s, g);
+  else if (nv <= 12) launch_gf<G, DPL, 12>(a, lds, s, g);
+  else if (nv <= 16) launch_gf<G, DPL, 16>(a, lds, s, g);
+  else if (G == 2 && nv <= 18) launch_gf<G, DPL, 18>(a, lds, s, g);
+  else return false;
+  return true;
+}
+#endif
+
 }  // namespace
 
 #if NFN_FAST
+// the Chain bijector (forward + fldj, chain_group1_kernel<..., FWD>) for d >= 4, contiguous rows
+bool launch_group1_fwd(int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid) {
+  if (G == 4 && DPL == 1) return launch_gf_nv<4, 1>(nv, a, lds, s, grid);
+  if (G == 4 && DPL == 2) return launch_gf_nv<4, 2>(nv, a, lds, s, grid);
+  if (G == 2 && DPL == 4) return launch_gf_nv<2, 4>(nv, a, lds, s, grid);
+  if (G == 4 && DPL == 4) return launch_gf_nv<4, 4>(nv, a, lds, s, grid);
+  if (G == 8 && DPL == 4) return launch_gf_nv<8, 4>(nv, a, lds, s, grid);
+  return false;
+}
+
 bool launch_group_fast(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
                        int64_t* grid) {
 #else

@@ -66,6 +66,8 @@ bool launch_group_fast(bool post, int G, int DPL, int nv, const ChainArgs& a, si
                        int64_t* grid);
 bool launch_group_precise(bool post, int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s,
                           int64_t* grid);
+// nfn_group.hip (fast-math unit): the Chain bijector for d >= 4 over contiguous layer rows
+bool launch_group1_fwd(int G, int DPL, int nv, const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid);
 // nfn_tile.hip
 void launch_tile(bool fast, bool post, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 void launch_chain_fwd_ldj(bool fast, int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, float* z_out,

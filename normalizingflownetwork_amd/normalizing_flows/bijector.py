@@ -131,16 +131,23 @@ class Chain(Bijector):
             return None
         storage0 = p0.untyped_storage().data_ptr()
         base = min(p.data_ptr() for p in ps)
-        # start the view at the 16-byte boundary at or before the leftmost block (within the
-        # storage): the layer's rows then stream as aligned float4 (the base columns to the
-        # left are staged, never read)
-        base = max(storage0, base - base % 16)
         if any((p.data_ptr() - base) % 4 for p in ps):
             return None
+        # start the view at the row start when the blocks are column views of whole rows
+        # (the layer's t: the kernels then stream contiguous rows), else at the 16-byte
+        # boundary at or before the leftmost block (aligned float4 rows); the columns left
+        # of the first block are staged, never read
+        rs = p0.stride(0) if p0.shape[0] > 1 else None
+        col = ((base - storage0) // 4) % rs if rs else None
+        if rs and base - 4 * col >= storage0:
+            base -= 4 * col
+        else:
+            base = max(storage0, base - base % 16)
         offs = [(p.data_ptr() - base) // 4 for p in ps]
         width = max(o + p.shape[1] for o, p in zip(offs, ps))
-        rs = p0.stride(0) if p0.shape[0] > 1 else width
-        if p0.shape[0] > 1 and width > rs:
+        if rs is None:
+            rs = width
+        elif width > rs:
             return None
         t = p0.as_strided((p0.shape[0], width), (rs, 1), (base - storage0) // 4)
         return [b.flow_type for b in flows], t, offs, flows[0].n_dims, ops
