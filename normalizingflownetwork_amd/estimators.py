@@ -214,7 +214,7 @@ class BaseEstimator:
             std = self.noise_scale_factor
         self.x_noise_std = self.y_noise_std = float(std)
 
-    def fit(self, x, y, batch_size=None, epochs=None, verbose=1, shuffle=True, **kwargs):
+    def fit(self, x, y, batch_size=None, epochs=None, verbose=1, shuffle=True, use_graph=True, **kwargs):
         """Maximum-likelihood training on the GPU: ``BaseEstimator.fit`` (``BaseEstimator.py:19-31``)
         with the model compiled as in ``MaximumLikelihoodNNEstimator.py:33-35`` —
         Adam(learning_rate), loss = mean over the batch of ``-log_prob(y_circ + noise | t)
@@ -222,7 +222,15 @@ class BaseEstimator:
         ``epochs=1``, per-epoch shuffling, GaussianNoise on the normalised x and y while
         training, and TerminateOnNaN.  ``t = MLP(x)`` runs in torch; ``log_prob`` and its
         gradient w.r.t. ``t`` run in the fused HIP kernels (``nfn_chain_logprob_f32`` /
-        ``nfn_chain_logprob_grad_f32``).  Returns ``{"loss": [per-epoch mean loss]}``."""
+        ``nfn_chain_logprob_grad_f32``).
+
+        At the reference's batch sizes a training step is a few dozen tiny launches, so with
+        ``use_graph`` the full-batch step (gather, normalisation, MLP, fused log_prob forward
+        and backward, Adam) is captured once into a HIP graph and replayed: per step only the
+        batch indices and the noise draws (if any) are written into the graph's static inputs
+        — the same generator calls in the same order as the eager loop, so both paths train
+        identically.  A final partial batch runs eagerly.  Returns ``{"loss": [per-epoch
+        mean loss]}``."""
         x = np.asarray(x, np.float32)
         y = np.asarray(y, np.float32)
         assert len(x.shape) == len(y.shape) == 2, "Please pass a matrix not a vector"
@@ -236,7 +244,9 @@ class BaseEstimator:
         nw = len(self._mlp.weights)
         self._mlp.weights, self._mlp.biases = params[:nw], params[nw:]
         lr = getattr(self, "learning_rate", 3e-3)
-        opt = torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-7)  # Keras Adam defaults
+        # Keras Adam defaults; capturable: the step counts and bias corrections live on the
+        # device, so the same optimizer runs eagerly and inside the graph
+        opt = torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-7, capturable=True)
         dl = self.dist_layer
         P = ops.total_param_size(dl.flow_types, self.n_dims, dl.trainable_base_dist)
         fused_dense = (len(self._mlp.weights) > 1 and self.fused_dense
@@ -249,33 +259,80 @@ class BaseEstimator:
         ym, ys = (torch.as_tensor(v, dtype=torch.float32, device=dev) for v in (self.y_mean, self.y_std))
         sum_log_ys = torch.log(ys).sum()
         gen = torch.Generator(device=dev).manual_seed(int(self.random_seed))
-        dl = self.dist_layer
         n = X.shape[0]
+        acc = torch.zeros((), dtype=torch.float64, device=dev)
+
+        def step(idx, nx, ny):
+            """One training step on the rows ``idx`` with the noise draws ``nx`` / ``ny``."""
+            xn = (X[idx] - xm) / (xs + 1e-8)
+            if nx is not None:
+                xn = xn + self.x_noise_std * nx
+            yc = (Y[idx] - ym) / ys
+            if ny is not None:
+                yc = yc + self.y_noise_std * ny
+            if fused_dense:  # output layer fused into the chain, forward and backward
+                lp = ops.log_prob_dense(yc, self._mlp.hidden(xn), self._mlp.weights[-1], self._mlp.biases[-1],
+                                        dl.flow_types, self.n_dims, dl.trainable_base_dist)
+            else:
+                t = self._mlp(xn)
+                lp = ops.log_prob(yc, t, dl.flow_types, self.n_dims, dl.trainable_base_dist)
+            loss = -lp.mean() + sum_log_ys
+            loss.backward()
+            opt.step()
+            acc.add_(loss.detach().double() * idx.numel())
+
+        def draws(rows):
+            nx = torch.randn((rows, X.shape[1]), generator=gen, device=dev) if self.x_noise_std > 0 else None
+            ny = torch.randn((rows, Y.shape[1]), generator=gen, device=dev) if self.y_noise_std > 0 else None
+            return nx, ny
+
+        graph = None  # (graph, static idx, static x noise, static y noise)
+        warm = 3  # eager steps before the capture (optimizer state, allocator pools)
+        steps_done = 0
         history = {"loss": []}
         try:
             for _ in range(epochs):
                 perm = torch.randperm(n, generator=gen, device=dev) if shuffle else torch.arange(n, device=dev)
-                acc = torch.zeros((), dtype=torch.float64, device=dev)
+                acc.zero_()
                 for i in range(0, n, batch_size):
                     idx = perm[i:i + batch_size]
-                    xn = (X[idx] - xm) / (xs + 1e-8)
-                    if self.x_noise_std > 0:
-                        xn = xn + self.x_noise_std * torch.randn(xn.shape, generator=gen, device=dev)
-                    yc = (Y[idx] - ym) / ys
-                    if self.y_noise_std > 0:
-                        yc = yc + self.y_noise_std * torch.randn(yc.shape, generator=gen, device=dev)
-                    if fused_dense:  # output layer fused into the chain, forward and backward
-                        lp = ops.log_prob_dense(yc, self._mlp.hidden(xn), self._mlp.weights[-1],
-                                                self._mlp.biases[-1], dl.flow_types, self.n_dims,
-                                                dl.trainable_base_dist)
-                    else:
-                        t = self._mlp(xn)
-                        lp = ops.log_prob(yc, t, dl.flow_types, self.n_dims, dl.trainable_base_dist)
-                    loss = -lp.mean() + sum_log_ys
+                    full = idx.numel() == batch_size
+                    if use_graph and full and graph is not None:
+                        g_, sidx, snx, sny = graph
+                        sidx.copy_(idx)
+                        if snx is not None:
+                            snx.normal_(generator=gen)
+                        if sny is not None:
+                            sny.normal_(generator=gen)
+                        g_.replay()
+                        continue
+                    nx, ny = draws(idx.numel())
+                    if use_graph and full and steps_done >= warm:
+                        # capture the full-batch step (the capture itself executes nothing:
+                        # this batch then runs as the graph's first replay)
+                        sidx = idx.clone()
+                        snx, sny = nx, ny
+                        opt.zero_grad(set_to_none=True)
+                        side = torch.cuda.Stream(device=dev)
+                        side.wait_stream(torch.cuda.current_stream(dev))
+                        g_ = torch.cuda.CUDAGraph()
+                        with torch.cuda.stream(side):
+                            with torch.cuda.graph(g_, stream=side):
+                                step(sidx, snx, sny)
+                        torch.cuda.current_stream(dev).wait_stream(side)
+                        graph = (g_, sidx, snx, sny)
+                        g_.replay()
+                        continue
                     opt.zero_grad(set_to_none=True)
-                    loss.backward()
-                    opt.step()
-                    acc += loss.detach().double() * idx.numel()
+                    if use_graph and steps_done < warm:
+                        side = torch.cuda.Stream(device=dev)  # warm-up on a side stream (capture rules)
+                        side.wait_stream(torch.cuda.current_stream(dev))
+                        with torch.cuda.stream(side):
+                            step(idx, nx, ny)
+                        torch.cuda.current_stream(dev).wait_stream(side)
+                    else:
+                        step(idx, nx, ny)
+                    steps_done += 1
                 ep_loss = float(acc.item()) / n
                 history["loss"].append(ep_loss)
                 if verbose:

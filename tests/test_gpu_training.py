@@ -189,3 +189,22 @@ def test_fit_fused_dense_matches_unfused(gpu):
     np.testing.assert_allclose(losses[True][:5], losses[False][:5], rtol=1e-5)
     np.testing.assert_allclose(losses[True][:10], losses[False][:10], rtol=5e-4)
     np.testing.assert_allclose(losses[True][-1], losses[False][-1], rtol=2e-2)
+
+
+@pytest.mark.parametrize("fused,noise", [(True, False), (False, True)])
+def test_fit_graph_replay_matches_eager(gpu, fused, noise):
+    """fit's HIP-graph path (the full-batch step captured once and replayed; a partial last
+    batch eager) trains exactly as the eager loop: same generator calls in the same order,
+    same kernels — the per-epoch losses and the final weights are bitwise equal."""
+    rng = np.random.default_rng(5)
+    x, y = _sinusoid(203, rng)  # 6 full batches of 32 + a partial one per epoch
+    out = {}
+    for use_graph in (True, False):
+        m = _nfn(1, n_flows=3, hidden_sizes=(16, 16), trainable_base_dist=True,
+                 noise_reg=("fixed_rate", 0.1 if noise else 0.0))
+        m.fused_dense = fused
+        hist = m.fit(x, y, epochs=4, verbose=0, use_graph=use_graph)["loss"]
+        out[use_graph] = (hist, [w.detach().cpu().numpy() for w in m._mlp.weights + m._mlp.biases])
+    assert out[True][0] == out[False][0]
+    for a, b in zip(out[True][1], out[False][1]):
+        np.testing.assert_array_equal(a, b)
