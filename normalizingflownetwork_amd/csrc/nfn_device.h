@@ -100,6 +100,7 @@ struct ChainArgs {
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
+  int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
   FlowProgram prog;
 };
 
@@ -1342,7 +1343,9 @@ __device__ __forceinline__ float gsum(float v) {
 // per-lane vector work (DPL dims each) and tile size.
 // FULL: d == G * DPL (every lane's dimensions exist; config C3), so the per-dimension
 // activity tests and their divergent branches compile away.
-template <int G, int DPL, bool FAST, bool FULL = false>
+// LDJ = false: the z step only (the backward's forward recompute when log_prob is not
+// wanted); returns 0.
+template <int G, int DPL, bool FAST, bool FULL = false, bool LDJ = true>
 __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int d_, int j) {
   const int d = FULL ? G * DPL : d_;
   float u[DPL], w[DPL];
@@ -1369,8 +1372,9 @@ __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int 
     for (int i = 0; i < DPL; ++i) {
       const float uh = fmaf(c2, w[i], u[i]);  // 0 on inactive dims
       z[i] = fmaf(uh, th, z[i]);
-      sd = fmaf(uh, w[i], sd);
+      if constexpr (LDJ) sd = fmaf(uh, w[i], sd);
     }
+    if constexpr (!LDJ) return 0.0f;
     return f_log<true>(fabsf(fmaf(fmaf(-th, th, 1.0f), gsum<G>(sd), 1.0f)));
   }
   const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
@@ -1388,7 +1392,7 @@ __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int 
   return f_log<FAST>(fabsf(1.0f + gsum<G>(sd)));
 }
 
-template <int G, int DPL, bool FAST, bool FULL = false>
+template <int G, int DPL, bool FAST, bool FULL = false, bool LDJ = true>
 __device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int d_, int j) {
   const int d = FULL ? G * DPL : d_;
   const float alpha = softplus_alpha<FAST>(0.3f * p[0] - 2.0f);
@@ -1411,6 +1415,7 @@ __device__ __forceinline__ float radial_gd(float (&z)[DPL], const float* p, int 
     for (int i = 0; i < DPL; ++i) {
       if (FULL || j + G * i < d) z[i] = fmaf(abh, z[i] - g[i], z[i]);
     }
+    if constexpr (!LDJ) return 0.0f;
     const float l2 = fmaf((float)(d - 1), __builtin_amdgcn_logf(1.0f + abh),
                           __builtin_amdgcn_logf(fmaf(abh, alpha * h, 1.0f)));
     return l2 * kLn2;

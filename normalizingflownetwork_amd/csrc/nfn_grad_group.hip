@@ -324,6 +324,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
     // forward, keeping each flow's input
     float ildj = 0.0f, dimterm = 0.0f;
     int off = P;
+    // without a log_prob output the forward recompute only needs each flow's input
+    // (z-only steps: no log-determinants)
+    const bool want_lp = a.out != nullptr || !a.zonly;
     for (int k = 0; k < K; ++k) {
       const int id = flow_type_at(tw, k);
       off -= flow_width(id, d);
@@ -331,16 +334,22 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
 #pragma unroll
       for (int i = 0; i < DPL; ++i) zh[(k * DPL + i) * 64] = z[i];
       if (id == NFN_FLOW_PLANAR) {
-        ildj = ildj + planar_gd<G, DPL, FAST, FULL>(z, p, d, j);
+        if (want_lp)
+          ildj = ildj + planar_gd<G, DPL, FAST, FULL>(z, p, d, j);
+        else
+          planar_gd<G, DPL, FAST, FULL, false>(z, p, d, j);
       } else if (id == NFN_FLOW_RADIAL) {
-        ildj = ildj + radial_gd<G, DPL, FAST, FULL>(z, p, d, j);
+        if (want_lp)
+          ildj = ildj + radial_gd<G, DPL, FAST, FULL>(z, p, d, j);
+        else
+          radial_gd<G, DPL, FAST, FULL, false>(z, p, d, j);
       } else {
 #pragma unroll
         for (int i = 0; i < DPL; ++i) {
           if (FULL || j + G * i < d) {
             const float s1 = 1.0f + p[d + j + G * i];
             z[i] = z[i] * s1 + p[j + G * i];
-            dimterm += f_log<FAST>(fabsf(s1));
+            if (want_lp) dimterm += f_log<FAST>(fabsf(s1));
           }
         }
       }

@@ -86,6 +86,7 @@ for s in $STEPS; do
     dense) run bench_dense 300 python bench.py --mode dense --steps 50 --warmup 10 --cpu-seconds 6 ;;
     densetests) run densetests 300 python -u -m pytest tests/test_gpu_dense.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     gradtests) run gradtests 300 python -u -m pytest tests/test_gpu_grad.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    grad_c3_nocpu) run bench_grad_c3 300 python bench.py --mode grad --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
     dgradmicro) run dgradmicro 300 python tools/microbench.py dgrad ;;
     prof_grad_c3)
       { cd /tmp; run rocprof_grad_c3 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof_grad_c3" -o gradc3 -- \
@@ -137,6 +138,8 @@ for s in $STEPS; do
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
+    gradc3) run gradc3 300 python tools/microbench.py gradc3 ;;
+    gradc3z) run gradc3z 300 python tools/microbench.py gradc3z ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -418,6 +418,12 @@ def main():
                         {"name": "wpb4_b", "env": {}}, {"name": "generic_walk_b", "env": {"NFN_GRAD_GROUP1": 0}},
                         {"name": "wpb2_b", "env": {"NFN_GRAD_GROUP_WPB": 2}}])
         return
+    if which[0] == "gradc3z":  # C3 backward: z-only forward recompute vs full flow steps
+        run_grad("C3", [{"name": "zonly", "env": {}}, {"name": "with_ldj", "env": {"NFN_GRAD_ZONLY": 0}},
+                        {"name": "zonly_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+                        {"name": "with_ldj_compute_only", "env": {"NFN_GRAD_ZONLY": 0, "NFN_ABLATE_LOADS": 1}},
+                        {"name": "zonly_b", "env": {}}, {"name": "with_ldj_b", "env": {"NFN_GRAD_ZONLY": 0}}])
+        return
     if which[0] == "grad":
         v = [{"name": "wave", "env": {}},
              {"name": "wpb4", "env": {"NFN_GRAD_WPB": 4}},
