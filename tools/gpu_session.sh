@@ -134,6 +134,7 @@ for s in $STEPS; do
     bijector_c3) run bench_bijector_c3 300 python bench.py --mode bijector --config C3 --steps 30 --warmup 5 --cpu-seconds 6 ;;
     fitbench) run fitbench 300 python tools/fit_bench.py ;;
     traintests) run traintests 400 python -u -m pytest tests/test_gpu_training.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    sweep) run sweep 300 python tools/microbench.py sweep ;;
     pcie) run pcie 300 python tools/microbench.py pcie ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;

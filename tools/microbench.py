@@ -356,8 +356,39 @@ def run_pcie(reps=5):
                           "h2d_bytes": B * (d + P) * 4 if name != "device_resident" else 0}), flush=True)
 
 
+def run_sweep(reps=30):
+    """Batch-size sweep of the C2 forward (fused log_prob + in-kernel fp64 sum): kernel time
+    with HIP events on the launch stream and the fraction of the 8 TB/s peak, B = 2^10..2^27
+    — where the chip saturates (small batches are launch / latency bound)."""
+    ft, d, _, _ = CFG["C2"]
+    P = ops.total_param_size(ft, d, True)
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    ymax = torch.randn((1 << 27, d), generator=gen, device="cuda")
+    tmax = torch.randn((1 << 27, P), generator=gen, device="cuda")
+    order = [int(v) for v in os.environ.get("NFN_SWEEP_ORDER", "").split(",") if v] or list(range(10, 28))
+    for e in order:
+        B = 1 << e
+        L = ops.ChainLauncher(ymax[:B], tmax[:B], ft, d, True)
+        prewarm(lambda: L.launch(sh), ms=100.0)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            L.launch(sh)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+        byts = B * (4 * d + 4 * P + 4)
+        print(json.dumps({"cfg": "C2", "mode": "sweep", "log2_batch": e, "ms": ms, "evals_per_s": B / ms * 1e3,
+                          "frac8TBs": byts / ms / 1e6 / 8000}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "sweep":
+        run_sweep()
+        return
     if which[0] == "pcie":
         run_pcie()
         return
