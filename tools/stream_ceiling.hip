@@ -272,16 +272,20 @@ int main() {
   {
     float* g2;
     CHECK(hipMalloc(&g2, tbytes));
-    for (int wpc : {1, 2, 3, 4}) {
+    for (int wpc : {1, 2, 3, 4, 6, 7}) {
       const int grid = cus * wpc;
       const double b = 2.0 * (double)tbytes;
       const float a0 = run_copy<0, 2>(t, g2, ntiles, sink, grid, 10);
       const float a1 = run_copy<1, 2>(t, g2, ntiles, sink, grid, 10);
       const float a2 = run_copy<0, 0>(t, g2, ntiles, sink, grid, 10);
       const float a3 = run_copy<1, 0>(t, g2, ntiles, sink, grid, 10);
+      const float a4 = run_copy<0, 16>(t, g2, ntiles, sink, grid, 10);
+      const float a5 = run_copy<0, 18>(t, g2, ntiles, sink, grid, 10);
       printf("copy (read 8 KiB + write 8 KiB per tile) wg/CU=%d | drained nt %.4f ms %.0f GB/s | pipelined nt %.4f ms "
-             "%.0f GB/s | drained def %.4f ms %.0f GB/s | pipelined def %.4f ms %.0f GB/s\n",
-             wpc, a0, b / a0 / 1e6, a1, b / a1 / 1e6, a2, b / a2 / 1e6, a3, b / a3 / 1e6);
+             "%.0f GB/s | drained def %.4f ms %.0f GB/s | pipelined def %.4f ms %.0f GB/s | drained sc1 %.4f ms %.0f GB/s"
+             " | drained sc1+nt %.4f ms %.0f GB/s\n",
+             wpc, a0, b / a0 / 1e6, a1, b / a1 / 1e6, a2, b / a2 / 1e6, a3, b / a3 / 1e6, a4, b / a4 / 1e6, a5,
+             b / a5 / 1e6);
       fflush(stdout);
     }
     CHECK(hipFree(g2));
