@@ -457,3 +457,35 @@ def test_chain_bijector_one_launch(name, d, gpu):
     for zz, ll in ((z, ldj), (z1, ldj1)):
         assert (np.abs(ll.cpu().numpy() - l64) <= np.maximum(1e-5 * np.maximum(1, np.abs(l64)), 8 * dl)).all()
         assert (np.abs(zz.cpu().numpy() - z64) <= np.maximum(1e-5 * np.maximum(1, np.abs(z64)), 8 * dz)).all()
+
+
+@pytest.mark.parametrize("ft,d,B", [(("planar", "radial"), 1, 65), (("radial",) * 14, 1, 1000),
+                                    (("affine", "planar"), 1, 1), (("planar", "radial") * 2, 4, 63),
+                                    (("radial", "planar", "affine"), 8, 257), (("planar",) * 20, 1, 130)])
+def test_chain_bijector_shapes(ft, d, B, gpu):
+    """The one-launch Chain over ragged batches and every kernel form it takes (d = 1 wave1
+    with Q = 2 / 16, a 16+-flow chain on the tile kernel, the d >= 4 lane groups): against the
+    flow-by-flow path within the oracle's fp32 spread (both fast-math forms of the same flows)."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+    from normalizingflownetwork_amd.normalizing_flows import Chain
+
+    rng = np.random.default_rng(B + d)
+    P = O.total_param_size(ft, d, True)
+    t = torch.from_numpy((0.5 * rng.standard_normal((B, P))).astype(np.float32)).cuda()
+    y = torch.from_numpy(rng.standard_normal((B, d)).astype(np.float32)).cuda()
+    chain = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d)
+    assert chain._fused() is not None
+    z, ldj = chain.forward_and_log_det_jacobian(y)
+    steps = Chain([type(b)(b.params.clone(), d) for b in chain.bijectors])
+    z1, ldj1 = steps.forward_and_log_det_jacobian(y)
+    _, blocks = O.split_params(t.cpu().numpy().astype(np.float64), ft, d, True)
+    zr, lr = y.cpu().numpy().astype(np.float64), np.zeros(B)
+    for f, tk in zip(ft, blocks):
+        zr, l = O.flow_forward_fldj(f, zr, tk, d)
+        lr = lr + l
+    for zz, ll in ((z, ldj), (z1, ldj1)):
+        assert zz.shape == (B, d) and ll.shape == (B,)
+        ez = np.abs(zz.cpu().numpy() - zr) / np.maximum(1.0, np.abs(zr))
+        el = np.abs(ll.cpu().numpy() - lr) / np.maximum(1.0, np.abs(lr))
+        assert ez.max() < 1e-4 and el.max() < 1e-4, (ez.max(), el.max())
+    assert (z - z1).abs().max().item() <= 1e-4 * max(1.0, z1.abs().max().item())
