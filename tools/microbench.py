@@ -384,8 +384,43 @@ def run_sweep(reps=30):
                           "frac8TBs": byts / ms / 1e6 / 8000}), flush=True)
 
 
+def run_slices(reps=10):
+    """Footprint vs launch length: the 2^27-sample C2 batch as ONE launch, as eight 2^24
+    launches over its eight consecutive slices (the same 17 GB, shorter launches), and one
+    2^24 launch repeated eight times over the first slice (2 GB footprint)."""
+    ft, d, _, _ = CFG["C2"]
+    P = ops.total_param_size(ft, d, True)
+    stream = torch.cuda.current_stream()
+    sh = int(stream.cuda_stream)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    ymax = torch.randn((1 << 27, d), generator=gen, device="cuda")
+    tmax = torch.randn((1 << 27, P), generator=gen, device="cuda")
+    big = ops.ChainLauncher(ymax, tmax, ft, d, True)
+    s24 = 1 << 24
+    parts = [ops.ChainLauncher(ymax[k * s24:(k + 1) * s24], tmax[k * s24:(k + 1) * s24], ft, d, True) for k in range(8)]
+    variants = {"one_2^27_launch": lambda: big.launch(sh),
+                "eight_2^24_slices": lambda: [p_.launch(sh) for p_ in parts],
+                "eight_2^24_same_slice": lambda: [parts[0].launch(sh) for _ in range(8)]}
+    prewarm(variants["one_2^27_launch"], ms=300.0)
+    for r in range(2):
+        for name, fn in variants.items():
+            fn()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in evs:
+                e0.record(stream)
+                fn()
+                e1.record(stream)
+            torch.cuda.synchronize()
+            ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+            print(json.dumps({"cfg": "C2", "mode": "slices", "round": r, "variant": name, "ms": ms,
+                              "frac8TBs": (1 << 27) * (4 * d + 4 * P + 4) / ms / 1e6 / 8000}), flush=True)
+
+
 def main():
     which = sys.argv[1:] or ["C2"]
+    if which[0] == "slices":
+        run_slices()
+        return
     if which[0] == "sweep":
         run_sweep()
         return
