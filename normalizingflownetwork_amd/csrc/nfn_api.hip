@@ -141,9 +141,25 @@ void group_shape(int dm, int want_g, int* G, int* DPL) {
 // workgroup of the smallest tile any launch uses (64 rows, fewer for very wide
 // rows).  Persistent launches whose grid could exceed it are capped at it
 // (ChainArgs::grid_cap), so no launch writes past the workspace.
-int64_t partials_capacity(int64_t B, int P) {
+int64_t raw_partials(int64_t B, int P) {
   const int rows = std::min(64, tile_geom(P < 0 ? 0 : P).rows);
   return (B + rows - 1) / rows;
+}
+
+// The plain chain runs a batch longer than this as consecutive launches over its
+// slices: the persistent grid's static tile stride drifts apart over a long launch
+// (C2 at 2^27 as one launch 3.33 ms, as eight 2^24 launches 2.90-3.01 ms).
+// Tuning knob NFN_CHUNK_LOG2 (0 = one launch), never below kMinChunkLog2.
+constexpr int kChunkLog2 = 24, kMinChunkLog2 = 20;
+int64_t chain_chunk_rows() {
+  const int l = env_int("NFN_CHUNK_LOG2", kChunkLog2);
+  return l <= 0 ? 0 : (int64_t)1 << std::max(l, kMinChunkLog2);
+}
+
+// Each chunk's grid is capped at raw_partials(chunk) slots, which exceed the slice's
+// share of raw_partials(B) by at most one: one spare slot per smallest chunk.
+int64_t partials_capacity(int64_t B, int P) {
+  return raw_partials(B, P) + (B >> kMinChunkLog2) + 1;
 }
 
 // Doubles of the [count | ticket | (sum, count) pairs] block.
@@ -165,11 +181,14 @@ int32_t check_hip(const char* what) {
   return NFN_OK;
 }
 
-int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride, int64_t t_rowstride,
-                  int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
-                  const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
-                  void* stream, bool posterior) {
-  g_last_error.clear();
+// One launch over B samples.  A chunk of a longer batch (chunk_cap > 0) writes its
+// partial pairs after the earlier chunks' (from slot pair_base, at most chunk_cap of
+// them); only the last chunk finishes out_sum, over every chunk's pairs.
+int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
+                         int64_t t_rowstride, int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
+                         int32_t trainable_base, const float* y_mean, const float* y_std, float* out,
+                         double* out_sum, double* workspace, void* stream, bool posterior, int64_t pair_base,
+                         int64_t chunk_cap, int64_t* grid_used) {
   ChainArgs a;
   memset(&a, 0, sizeof(a));
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
@@ -206,7 +225,8 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
   a.out = out;
   a.partials = workspace ? workspace + 2 : nullptr;  // [count | ticket | pairs]
   a.out_sum = workspace ? out_sum : nullptr;         // finished in-kernel by the last workgroup
-  a.grid_cap = workspace ? partials_capacity(B, P) : 0;
+  a.grid_cap = workspace ? (chunk_cap > 0 ? chunk_cap : partials_capacity(B, P)) : 0;
+  a.pair_base = pair_base;
   a.y_bstride = y_bstride;
   a.t_rowstride = t_rowstride;
   a.t_drawstride = t_drawstride;
@@ -304,7 +324,34 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
     const dim3 grid((unsigned)nblk), block((unsigned)g.threads);
     launch_tile(use_fast_math(), posterior, dm, a, grid, block, g.lds_bytes, s);
   }
+  if (grid_used) *grid_used = nblk;
   return check_hip(posterior ? "posterior kernel launch" : "chain kernel launch");
+}
+
+int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride, int64_t t_rowstride,
+                  int32_t S, int64_t B, int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base,
+                  const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
+                  void* stream, bool posterior) {
+  g_last_error.clear();
+  const int64_t chunk = posterior ? 0 : chain_chunk_rows();
+  if (chunk <= 0 || B <= chunk || !y || (t == nullptr && t_rowstride != 0))
+    return run_chain_launch(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, flow_ids, K, trainable_base, y_mean,
+                            y_std, out, out_sum, workspace, stream, posterior, 0, 0, nullptr);
+  const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, nullptr);
+  if (P < 0) return P;
+  int64_t base = 0;
+  for (int64_t b0 = 0; b0 < B; b0 += chunk) {
+    const int64_t nb = std::min(chunk, B - b0);
+    const bool last = b0 + nb >= B;
+    int64_t used = 0;
+    const int32_t rc = run_chain_launch(y + b0 * y_bstride, y_bstride, t ? t + b0 * t_rowstride : nullptr, t_drawstride,
+                                        t_rowstride, S, nb, d, flow_ids, K, trainable_base, y_mean, y_std,
+                                        out ? out + b0 : nullptr, last ? out_sum : nullptr, workspace, stream, false,
+                                        base, raw_partials(nb, P), &used);
+    if (rc != NFN_OK) return rc;
+    base += used;
+  }
+  return NFN_OK;
 }
 
 int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride, int64_t B, int32_t d,

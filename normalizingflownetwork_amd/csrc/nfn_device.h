@@ -101,6 +101,7 @@ struct ChainArgs {
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
+  int64_t pair_base;   // chunked batch: this launch's first partial slot (earlier chunks' pairs precede it)
   FlowProgram prog;
 };
 
@@ -696,7 +697,7 @@ __device__ __forceinline__ void sum_pairs(const double* __restrict__ pairs, int6
 // whole L2 in every workgroup.  The ticket is a vector atomic.  `red` holds
 // 2 * kMaxBlock / 64 doubles.  Contains __syncthreads: call from every thread.
 __device__ __forceinline__ void write_partial(double* partials, double acc, int nf, double* red,
-                                              double* out_sum) {
+                                              double* out_sum, int64_t base = 0) {
   double c = (double)nf;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -716,9 +717,10 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
       s += red[2 * w];
       n += red[2 * w + 1];
     }
-    __hip_atomic_store(partials + 2 * blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(partials + 2 * blockIdx.x + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (blockIdx.x == 0) partials[-2] = (double)gridDim.x;  // workspace header: number of pairs
+    const int64_t slot = base + blockIdx.x;
+    __hip_atomic_store(partials + 2 * slot, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partials + 2 * slot + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0) partials[-2] = (double)(base + gridDim.x);  // workspace header: number of pairs
   }
   if (out_sum == nullptr) return;  // partials-only launch (nfn_reduce_partials_f64 finishes it)
   unsigned* ticket = reinterpret_cast<unsigned*>(partials - 1);
@@ -733,7 +735,7 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
   const bool last = flag[0] != 0;
   __syncthreads();
   if (!last) return;
-  sum_pairs<true>(partials, gridDim.x, red, out_sum);
+  sum_pairs<true>(partials, base + gridDim.x, red, out_sum);
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -763,7 +765,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
     lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
     if (a.out) a.out[b] = lp;
   }
-  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red, a.out_sum);
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red, a.out_sum, a.pair_base);
 }
 
 // Posterior: the same tile walk once per draw, with an online logsumexp over draws.
@@ -800,7 +802,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
     res = lse_finish<FAST>(m, acc, a.S);
     if (a.out) a.out[b0 + tid] = res;
   }
-  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red, a.out_sum);
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red, a.out_sum, a.pair_base);
 }
 
 // Persistent, software-pipelined version of the two kernels above (the hot path).
@@ -1009,7 +1011,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     }
   }
   if (a.partials && (!POST || nsp == 1)) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
   }
 }
 
@@ -1135,7 +1137,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   }
   flush();
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
   }
 }
 
@@ -1267,7 +1269,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs
     rg = rgn;
   }
   flush();
-  if (a.partials && nsp == 1) write_partial(a.partials, acc_sum, nfc, red, a.out_sum);
+  if (a.partials && nsp == 1) write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.pair_base);
 }
 
 // Combines the per-range (max, scaled sum) pairs of a draw-split posterior:
@@ -1630,7 +1632,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   }
   if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
   }
 }
 
@@ -1741,7 +1743,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   }
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
   }
 }
 

@@ -198,8 +198,8 @@ def test_concurrent_streams_match_single_stream(gpu):
 
 
 def test_c4_global_batch_on_one_device(gpu):
-    """2^27 samples (C4's global batch) in one launch: t is 16 GiB, element offsets pass
-    2^31.  Samples spread over the whole batch (and the last rows) against the oracle;
+    """2^27 samples (C4's global batch) in one call (eight 2^24-sample launches): t is
+    16 GiB, element offsets pass 2^31.  Samples spread over the whole batch (and the last rows) against the oracle;
     the fused sum and the non-finite count against the returned values."""
     from normalizingflownetwork_amd import ops
 
@@ -220,6 +220,69 @@ def test_c4_global_batch_on_one_device(gpu):
     r64 = O.chain_log_prob(yn, tn, C2, 1, True, np.float64)
     r32 = O.chain_log_prob(yn, tn, C2, 1, True, np.float32)
     got = lp[idx].cpu().numpy().astype(np.float64)
+    ok = np.isfinite(r64)
+    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    del t
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("ft,d,B", [(C2, 1, (1 << 24) + 4097), (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8,
+                                                                 (1 << 24) + 999)])
+def test_chunked_batch(ft, d, B, gpu):
+    """A batch past 2^24 samples runs as consecutive launches over its slices (the
+    static tile stride drifts over one long launch).  Values bitwise those of
+    separate calls on the slices; one fused sum over every chunk's partials (the same
+    bits as the partials-only call + nfn_reduce_partials_f64), the workspace not overrun,
+    the ticket left at zero, the header = the total number of pairs."""
+    from normalizingflownetwork_amd import _lib
+
+    lib = _lib.load()
+    P = O.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(B)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    t = 0.5 * torch.randn((B, P), generator=gen, device="cuda")
+    ids, k = _ids(ft)
+    n = int(lib.nfn_chain_workspace_doubles(B, d, P))
+    ws = _canary_ws(n)
+    out = torch.empty((B,), dtype=torch.float32, device="cuda")
+    osum = torch.empty((2,), dtype=torch.float64, device="cuda")
+
+    def call(yv, tv, nb, o, s, w):
+        rc = lib.nfn_chain_logprob_f32(yv.data_ptr(), d, tv.data_ptr(), P, nb, d, ctypes.cast(ids, ctypes.c_void_p), k,
+                                       1, None, None, o.data_ptr() if o is not None else None,
+                                       s.data_ptr() if s is not None else None, w.data_ptr() if w is not None else None,
+                                       None)
+        _lib.check(rc, "chain")
+
+    call(y, t, B, out, osum, ws)
+    torch.cuda.synchronize()
+    _check_canary(ws, n, f"chunked d={d} B={B}")
+    assert int(ws[1].item()) == 0
+    npairs = int(ws[0].item())
+    assert 2 <= npairs <= (n - 2) // 2
+    assert float(osum[0].item()) == pytest.approx(out.double().sum().item(), rel=1e-12)
+    assert osum[1].item() == float((~torch.isfinite(out)).sum().item())
+    # partials-only call, then the reduction: the same bits
+    ws2 = torch.zeros((n,), dtype=torch.float64, device="cuda")
+    call(y, t, B, None, None, ws2)
+    osum2 = torch.empty((2,), dtype=torch.float64, device="cuda")
+    _lib.check(lib.nfn_reduce_partials_f64(ws2.data_ptr(), osum2.data_ptr(), None), "reduce")
+    torch.cuda.synchronize()
+    assert int(ws2[0].item()) == npairs
+    assert torch.equal(osum2, osum)
+    # each slice on its own: bitwise the same values
+    c = 1 << 24
+    for b0 in (0, c):
+        nb = min(c, B - b0)
+        o = torch.empty((nb,), dtype=torch.float32, device="cuda")
+        call(y[b0:], t[b0:], nb, o, None, None)
+        assert torch.equal(o, out[b0:b0 + nb])
+    idx = torch.cat([torch.arange(c - 300, c + 300, device="cuda"), torch.arange(B - 200, B, device="cuda"),
+                     torch.randint(0, B, (1000,), generator=gen, device="cuda")])
+    yn, tn = y[idx].cpu().numpy(), t[idx].cpu().numpy()
+    r64 = O.chain_log_prob(yn, tn, ft, d, True, np.float64)
+    r32 = O.chain_log_prob(yn, tn, ft, d, True, np.float32)
+    got = out[idx].cpu().numpy().astype(np.float64)
     ok = np.isfinite(r64)
     assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
     del t

@@ -135,6 +135,8 @@ for s in $STEPS; do
     fitbench) run fitbench 300 python tools/fit_bench.py ;;
     traintests) run traintests 400 python -u -m pytest tests/test_gpu_training.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep) run sweep 300 python tools/microbench.py sweep ;;
+    slices) run slices 300 python tools/microbench.py slices ;;
+    wstests) run wstests 400 python -u -m pytest tests/test_gpu_workspace.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     pcie) run pcie 300 python tools/microbench.py pcie ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;

@@ -398,10 +398,16 @@ def run_slices(reps=10):
     big = ops.ChainLauncher(ymax, tmax, ft, d, True)
     s24 = 1 << 24
     parts = [ops.ChainLauncher(ymax[k * s24:(k + 1) * s24], tmax[k * s24:(k + 1) * s24], ft, d, True) for k in range(8)]
-    variants = {"one_2^27_launch": lambda: big.launch(sh),
+    def unchunked():
+        os.environ["NFN_CHUNK_LOG2"] = "0"  # one launch over the whole batch (diag build)
+        big.launch(sh)
+        os.environ.pop("NFN_CHUNK_LOG2")
+
+    variants = {"one_2^27_call_chunked": lambda: big.launch(sh),
+                "one_2^27_launch_unchunked": unchunked,
                 "eight_2^24_slices": lambda: [p_.launch(sh) for p_ in parts],
                 "eight_2^24_same_slice": lambda: [parts[0].launch(sh) for _ in range(8)]}
-    prewarm(variants["one_2^27_launch"], ms=300.0)
+    prewarm(variants["one_2^27_call_chunked"], ms=300.0)
     for r in range(2):
         for name, fn in variants.items():
             fn()
