@@ -138,6 +138,9 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *                With out_sum == NULL and workspace != NULL only the pairs are written
  *                (finish with nfn_reduce_partials_f64).  One workspace per call in
  *                flight: two calls in flight sharing one race.
+ * A batch longer than 2^24 samples runs as consecutive launches over 2^24-sample slices
+ * (a long persistent launch drifts): their pairs follow one another in the
+ * workspace, n counts them all, and out_sum is one sum over every pair in fixed order.
  */
 int32_t nfn_chain_logprob_f32(const float* y, int64_t y_bstride, const float* t, int64_t t_rowstride,
                               int64_t B, int32_t d, const int32_t* flow_ids, int32_t K,
