@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
 // after the next prefetch, no branch between a load and its use.  QH = H / 4.
 // NN = 16-column N tiles of t (P <= 16 NN), a compile-time count so the GEMM unrolls
 // and the tile's A fragments are read from LDS once for all N tiles.
-template <int QH, int NN>
+template <int QH, int NN, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
       }
     }
     wave_lds_sync();
-    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS>(z0, tl + lane, a)
+    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM>(z0, tl + lane, a)
                                      : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
     if (lane < nr) {
       acc_sum += (double)lp;
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
 // W / bias fragments are prefetched (buffer loads, counted waits) while the current
 // unit runs the MFMA GEMM and the chain; the tile's result leaves once, after its
 // last draw (the per-unit store of the other draws goes through an empty descriptor).
-template <int QH, int NN>
+template <int QH, int NN, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
         }
       }
       wave_lds_sync();
-      const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS>(z0, tl + lane, a)
+      const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM>(z0, tl + lane, a)
                                        : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
       lse_push<true>(m, lacc, lp);
       wave_lds_sync();  // this unit's LDS reads done before the next unit's writes
@@ -527,9 +527,16 @@ template <int QH>
 void launch_pd1(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
   const size_t lds = (size_t)(4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
-  auto kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1>
-                     : (nn == 2 ? posterior_dense1_kernel<QH, 2> : (nn == 3 ? posterior_dense1_kernel<QH, 3>
-                                                                            : posterior_dense1_kernel<QH, 4>));
+  constexpr int CM = kChainPairs;
+  auto kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1, CM>
+                     : (nn == 2 ? posterior_dense1_kernel<QH, 2, CM> : (nn == 3 ? posterior_dense1_kernel<QH, 3, CM>
+                                                                                : posterior_dense1_kernel<QH, 4, CM>));
+#ifdef NFN_DIAG
+  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop)
+    kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1>
+                  : (nn == 2 ? posterior_dense1_kernel<QH, 2> : (nn == 3 ? posterior_dense1_kernel<QH, 3>
+                                                                         : posterior_dense1_kernel<QH, 4>));
+#endif
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
@@ -571,9 +578,16 @@ template <int QH>
 void launch_d1(const DenseArgs& da, size_t /*generic kernel's LDS*/, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
   const size_t lds = (size_t)(4 * QH * nn * 16 + 4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
-  auto kfn = nn <= 1 ? chain_dense1_kernel<QH, 1>
-                     : (nn == 2 ? chain_dense1_kernel<QH, 2> : (nn == 3 ? chain_dense1_kernel<QH, 3>
-                                                                       : chain_dense1_kernel<QH, 4>));
+  constexpr int CM = kChainPairs;
+  auto kfn = nn <= 1 ? chain_dense1_kernel<QH, 1, CM>
+                     : (nn == 2 ? chain_dense1_kernel<QH, 2, CM> : (nn == 3 ? chain_dense1_kernel<QH, 3, CM>
+                                                                           : chain_dense1_kernel<QH, 4, CM>));
+#ifdef NFN_DIAG
+  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop)
+    kfn = nn <= 1 ? chain_dense1_kernel<QH, 1>
+                  : (nn == 2 ? chain_dense1_kernel<QH, 2> : (nn == 3 ? chain_dense1_kernel<QH, 3>
+                                                                    : chain_dense1_kernel<QH, 4>));
+#endif
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);

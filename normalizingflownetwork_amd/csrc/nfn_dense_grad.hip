@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradAr
 // Per wave LDS: the t tile ((P + 2) columns, the packed reverse pass reads up to two
 // past the last block) and the flow inputs z_k.  Every workgroup writes one partial
 // [dW | db], summed across waves in wave order: bitwise deterministic.
-template <int MH, int NN>
+template <int MH, int NN, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradArgs g) {
   const DenseArgs& da = g.da;
   const ChainArgs& a = da.c;
@@ -380,7 +380,11 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
     wave_lds_sync();
     // 3. the chain forward + reverse per lane: the t column entries become g * d logp / d t
     float adj, z = z0;
-    const float lp = grad1_packed<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
+    float lp;
+    if constexpr (CM == kChainPairs)
+      lp = grad1_pairs<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
+    else
+      lp = grad1_packed<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
     if (nr < 64 && lane >= nr) {  // rows past B carry no gradient
       for (int p = 0; p < P; ++p) tl[p * kCS + lane] = 0.0f;
     }
@@ -490,7 +494,10 @@ __global__ void __launch_bounds__(1024) sum_partials_kernel(const float* __restr
 
 template <int MH, int NN>
 int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
-  auto kfn = chain_dense1_grad_kernel<MH, NN>;
+  auto kfn = chain_dense1_grad_kernel<MH, NN, kChainPairs>;
+#ifdef NFN_DIAG
+  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop) kfn = chain_dense1_grad_kernel<MH, NN>;
+#endif
   const size_t lds = (size_t)4 * dense1_grad_wave_floats(g.da.c.P, 16 * MH + 4, g.da.c.prog.K) * sizeof(float);
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, max_parts));

@@ -530,6 +530,93 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
   return l2;
 }
 
+// A program fixed at compile time (TYPES, K): straight-line code, no dispatch.
+template <uint32_t TYPES, int K, int ST = 1>
+__device__ __forceinline__ float chain1_fast_static(float& z, const float* row, int P) {
+  float l2 = 0.0f;
+  int off = P;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int id = (int)((TYPES >> (2 * k)) & 3u);
+    off -= size1(id);
+    float pc[3];
+    read3c<ST>(pc, row, off);
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+  }
+  return l2;
+}
+
+// Two flows per dispatch: each of the nine (type, type) pairs is straight-line code,
+// so the second flow's parameter-only work (softplus, u_hat, alpha, beta) can issue
+// under the first flow's z chain, and the type dispatch runs once per pair.  The
+// next pair's parameters are read (LDS) before the current pair is evaluated.
+template <int IA, int IB>
+__device__ __forceinline__ void flow_pair1(float& z, float& l2, const float (&pa)[3], const float (&pb)[3]) {
+  const float da = flow1_fast(IA, z, pa);
+  l2 += __builtin_amdgcn_logf(fabsf(da));
+  const float db = flow1_fast(IB, z, pb);
+  l2 += __builtin_amdgcn_logf(fabsf(db));
+}
+
+#define NFN_PAIR_SWITCH(sel, CALL) \
+  switch (sel) {                   \
+    case 0: CALL(0, 0); break;     \
+    case 1: CALL(0, 1); break;     \
+    case 2: CALL(0, 2); break;     \
+    case 3: CALL(1, 0); break;     \
+    case 4: CALL(1, 1); break;     \
+    case 5: CALL(1, 2); break;     \
+    case 6: CALL(2, 0); break;     \
+    case 7: CALL(2, 1); break;     \
+    default: CALL(2, 2); break;    \
+  }
+
+// Flow k's type; flows past the program read as planar (offsets then clamp at 0:
+// harmless in-row reads of the padded tile).
+__device__ __forceinline__ int type1(uint32_t types, int k) { return (int)((types >> ((2 * k) & 31)) & 3u); }
+
+template <int ST = 1>
+__device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, uint32_t types, int K, int P) {
+  float l2 = 0.0f;
+  int ia = type1(types, 0), ib = type1(types, 1);
+  int offa = max(P - size1(ia), 0), offb = max(offa - size1(ib), 0);
+  float pa[3], pb[3];
+  read3c<ST>(pa, row, offa);
+  read3c<ST>(pb, row, offb);
+#pragma unroll 1
+  for (int k = 0; k + 1 < K; k += 2) {
+    const int ian = type1(types, k + 2), ibn = type1(types, k + 3);
+    const int offan = max(offb - size1(ian), 0), offbn = max(offan - size1(ibn), 0);
+    float pna[3], pnb[3];
+    read3c<ST>(pna, row, offan);
+    read3c<ST>(pnb, row, offbn);
+#define NFN_FWD(A, B) flow_pair1<A, B>(z, l2, pa, pb)
+    NFN_PAIR_SWITCH(ia * 3 + ib, NFN_FWD)
+#undef NFN_FWD
+    ia = ian;
+    ib = ibn;
+    offb = offbn;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pa[i] = pna[i];
+      pb[i] = pnb[i];
+    }
+  }
+  if (K & 1) l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(ia, z, pa)));  // the last flow: already read
+  return l2;
+}
+
+// Chain-evaluation form of the d = 1 kernels: the packed loop, two flows per dispatch,
+// or (diagnostic experiment) one compile-time program, C2's.
+constexpr int kChainLoop = 0, kStaticProg = 2, kChainPairs = 3;
+// The pair form is bitwise the loop's.  It runs in the compute-bound d = 1 kernels
+// (posterior, fused Dense forward / backward: -5 to -11 %) and, in the streaming
+// kernels, for chains of at most this many flows (C1, K = 2: forward -18 %, backward
+// -11 %); at K = 10 (C2) the streaming kernels stream 3-7 % slower with it.
+constexpr int kPairsMaxKStream = 4;
+constexpr uint32_t kStaticTypes[] = {0x44444u};  // (planar, radial) x 5
+constexpr int kStaticK[] = {10};
+
 // Base log-density at d = 1 (fast math), shared by every d = 1 evaluator.
 template <int ST = 1>
 __device__ __forceinline__ float base1_fast(float z, const float* row, bool trainable) {
@@ -541,11 +628,15 @@ __device__ __forceinline__ float base1_fast(float z, const float* row, bool trai
   return -0.5f * (z * z) - kHalfLog2Pi;
 }
 
-template <bool PACKED, int ST = 1>
+template <bool PACKED, int ST = 1, int CM = kChainLoop>
 __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, const ChainArgs& a) {
   const int K = a.prog.K;
   float l2 = 0.0f;  // sum of log2|det J_k|
-  if constexpr (PACKED) {
+  if constexpr (CM == kChainPairs) {
+    if (K > 0) l2 = chain1_fast_pairs<ST>(z, row, a.prog.types[0], K, a.P);
+  } else if constexpr (CM == kStaticProg) {
+    l2 = chain1_fast_static<kStaticTypes[0], kStaticK[0], ST>(z, row, a.P);
+  } else if constexpr (PACKED) {
     if (K > 0) l2 = chain1_fast_packed<ST>(z, row, a.prog.types[0], K, a.P);
   } else if (K > 0) {
     int st = a.prog.step[0];
@@ -1035,7 +1126,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
 // FWD: the Bijector API's Chain forward + forward_log_det_jacobian instead of log_prob
 // (nfn_chain_fwd_ldj_f32 over the layer's flow blocks; needs FAST and PACKED): z_K goes to
 // a.z_out and sum_k log|det J_k| to a.out; no base density, no partial sums.
-template <bool FAST, int Q, bool PACKED, bool FWD = false>
+template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
@@ -1122,7 +1213,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       pend_z = z;
       pend_rz = tile_rsrc(a.z_out && nr > 0 ? a.z_out + b0 : a.z_out, a.z_out ? nr * 4 : 0);
     } else if constexpr (FAST) {
-      lp = eval_chain1_fast<PACKED>(z0, tl + lane * S, a) - corr;
+      lp = eval_chain1_fast<PACKED, 1, CM>(z0, tl + lane * S, a) - corr;
     } else {
       float z[1] = {z0};
       lp = eval_chain<1, false>(z, tl + lane * S, a) - corr;
@@ -1153,7 +1244,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
 // nsplit == 1 (enough tiles for every resident wave: C5 at 2^17 samples) a unit is a
 // whole tile, its score leaves once and there is no merge pass; otherwise units write
 // (max, scaled sum) pairs for posterior_merge_kernel.
-template <int Q, bool PACKED>
+template <int Q, bool PACKED, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
@@ -1248,7 +1339,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs
       flush();
       pend_r = empty_r;
       if (a.prio) __builtin_amdgcn_s_setprio(0);
-      const float lp = eval_chain1_fast<PACKED>(z0, tl + lane * LS, a) - corr;
+      const float lp = eval_chain1_fast<PACKED, 1, CM>(z0, tl + lane * LS, a) - corr;
       lse_push<true>(m, lacc, lp);
       wave_lds_sync();  // this draw's LDS reads done before the next draw's writes
     }

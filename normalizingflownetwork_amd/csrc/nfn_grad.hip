@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(64) chain_grad_kernel(GradArgs ga) {
 // registers (non-temporal) while the current tile runs forward + reverse; the
 // gradient tile is then written back from LDS with coalesced non-temporal
 // float4 stores (lane -> (row, 16-byte column) as for the loads).
-template <int DM, bool FAST, int NV, int MINW>
+template <int DM, bool FAST, int NV, int MINW, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradArgs ga) {
   const ChainArgs& a = ga.c;
   extern __shared__ float lds[];
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
     if (lane < nr) {
       const int64_t b = b0 + lane;
       float adj[DM];
-      const float lp = grad_sample<DM, FAST>(z, tl + lane * S, zh, 64, a, gl, adj) - corr;
+      const float lp = grad_sample<DM, FAST, CM>(z, tl + lane * S, zh, 64, a, gl, adj) - corr;
       if (a.out) __builtin_nontemporal_store(lp, a.out + b);
       if (ga.grad_y) store_grad_y<DM, FAST>(ga, b, adj);
     }
@@ -200,6 +200,10 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
   auto k = chain_grad_wave_kernel<DM, FAST, NV, 1>;
   if constexpr (DM == 1 && NV == 8) {
     if (env_int("NFN_GRAD_CAP", 0) == 1) k = chain_grad_wave_kernel<DM, FAST, NV, 4>;
+  }
+  if constexpr (DM == 1 && FAST) {
+    const int cm = env_int("NFN_CHAIN_FORM", ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop);
+    if (cm == kChainPairs && env_int("NFN_GRAD_CAP", 0) != 1) k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainPairs>;
   }
   const int T = 64 * waves_per_block;
   const int64_t teams = persistent_grid(k, T, lds_block, (ga.c.ntiles + waves_per_block - 1) / waves_per_block);

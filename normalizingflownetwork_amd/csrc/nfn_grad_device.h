@@ -373,6 +373,138 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
 }
 
 
+// grad1_packed with two flows per dispatch in both passes (chain1_fast_pairs): each of
+// the nine (type, type) bodies is straight-line code.  Same arithmetic in the same
+// order as grad1_packed.
+__device__ __forceinline__ void flow1_z(int id, float& z, const float (&p)[3]) {
+  if (id == NFN_FLOW_PLANAR)
+    planar1_z(z, p[0], p[1], p[2]);
+  else if (id == NFN_FLOW_RADIAL)
+    radial1_z(z, p[0], p[1], p[2]);
+  else
+    z = fmaf(z, 1.0f + p[1], p[0]);
+}
+
+template <int IA, int IB>
+__device__ __forceinline__ void fwd_pair1(float& z, float& l2, float& za, float& zb, const float (&pa)[3],
+                                          const float (&pb)[3], bool want_lp) {
+  za = z;
+  if (want_lp)
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+  else
+    flow1_z(IA, z, pa);
+  zb = z;
+  if (want_lp)
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IB, z, pb)));
+  else
+    flow1_z(IB, z, pb);
+}
+
+template <int IA, int IB, int ST>
+__device__ __forceinline__ void bwd_pair1(float& a1, float* row, float za, float zb, const float (&pa)[3],
+                                          const float (&pb)[3], int oba, int obb, float gl) {
+  flow1_bwd<ST>(IA, za, a1, pa, row + oba * ST, gl);
+  flow1_bwd<ST>(IB, zb, a1, pb, row + obb * ST, gl);
+}
+
+template <int ST = 1>
+__device__ __forceinline__ float grad1_pairs(float& z, float* row, float* zh, int zs, uint32_t types, int K, int P,
+                                             bool trainable, float gl, bool want_lp, float& adj) {
+  float l2 = 0.0f;
+  int ia = type1(types, 0), ib = type1(types, 1);
+  int offa = max(P - size1(ia), 0), offb = max(offa - size1(ib), 0);
+  float pa[3] = {0.0f, 0.0f, 0.0f}, pb[3] = {0.0f, 0.0f, 0.0f};
+  if (K > 0) {
+    read3c<ST>(pa, row, offa);
+    read3c<ST>(pb, row, offb);
+  }
+  int k = 0;
+#pragma unroll 1
+  for (; k + 1 < K; k += 2) {
+    const int ian = type1(types, k + 2), ibn = type1(types, k + 3);
+    const int offan = max(offb - size1(ian), 0), offbn = max(offan - size1(ibn), 0);
+    float pna[3], pnb[3];
+    read3c<ST>(pna, row, offan);
+    read3c<ST>(pnb, row, offbn);
+    float za, zb;
+#define NFN_FWD(A, B) fwd_pair1<A, B>(z, l2, za, zb, pa, pb, want_lp)
+    NFN_PAIR_SWITCH(ia * 3 + ib, NFN_FWD)
+#undef NFN_FWD
+    zh[k * zs] = za;
+    zh[(k + 1) * zs] = zb;
+    ia = ian;
+    ib = ibn;
+    offb = offbn;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pa[i] = pna[i];
+      pb[i] = pnb[i];
+    }
+  }
+  if (K & 1) {  // the last flow: already read
+    zh[(K - 1) * zs] = z;
+    if (want_lp)
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(ia, z, pa)));
+    else
+      flow1_z(ia, z, pa);
+  }
+  const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  float a1;
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[ST], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    a1 = -gz;
+    row[0] = gz;
+    row[ST] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+  } else {
+    a1 = -gl * z;
+  }
+  // reverse, flows K-1, K-2, ... in pairs: flow K-1's block follows the base, flow
+  // k-1's follows flow k's; the next pair's parameters and inputs are read first
+  k = K - 1;
+  ia = type1(types, k);
+  ib = type1(types, k - 1);
+  int oba = min(trainable ? 2 : 0, P - 1);
+  int obb = min(oba + size1(ia), P - 1);
+  float za = 0.0f, zb = 0.0f;
+  if (K > 0) {
+    read3c<ST>(pa, row, oba);
+    read3c<ST>(pb, row, obb);
+    za = zh[k * zs];
+    zb = zh[max(k - 1, 0) * zs];
+  }
+#pragma unroll 1
+  for (; k >= 1; k -= 2) {
+    const int ian = type1(types, k - 2), ibn = type1(types, k - 3);
+    const int oban = min(obb + size1(ib), P - 1), obbn = min(oban + size1(ian), P - 1);
+    float pna[3], pnb[3];
+    read3c<ST>(pna, row, oban);
+    read3c<ST>(pnb, row, obbn);
+    const float zan = zh[max(k - 2, 0) * zs], zbn = zh[max(k - 3, 0) * zs];
+#define NFN_BWD(A, B) bwd_pair1<A, B, ST>(a1, row, za, zb, pa, pb, oba, obb, gl)
+    NFN_PAIR_SWITCH(ia * 3 + ib, NFN_BWD)
+#undef NFN_BWD
+    ia = ian;
+    ib = ibn;
+    oba = oban;
+    obb = obbn;
+    za = zan;
+    zb = zbn;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pa[i] = pna[i];
+      pb[i] = pnb[i];
+    }
+  }
+  if (k == 0) flow1_bwd<ST>(ia, za, a1, pa, row + oba * ST, gl);  // flow 0: already read
+  adj = a1;
+  return lp;
+}
+
+
 // ---------------------------------------------------------------------------
 // Lane-group forms (d >= 4): a G-lane group owns one sample, lane j holds the
 // DPL dimensions j, j + G, ...; inner products are DPP group sums (gsum).
@@ -551,7 +683,7 @@ __device__ __forceinline__ void base_gd_bwd(const float (&z)[DPL], float (&a)[DP
 // zh[(k * d + j) * zs] (LDS), then the reverse pass; the parameter row `row` (LDS)
 // is overwritten in place with d logp / d t.  Returns log_prob (without the
 // -sum(log y_std) correction); `adj` receives d logp / d z_0.
-template <int DM, bool FAST>
+template <int DM, bool FAST, int CM = kChainLoop>
 __device__ __forceinline__ float grad_sample(float (&z)[DM], float* row, float* zh, int zs, const ChainArgs& a,
                                              float gl, float (&adj)[DM]) {
   const int d = a.d;
@@ -560,8 +692,10 @@ __device__ __forceinline__ float grad_sample(float (&z)[DM], float* row, float* 
   if constexpr (DM == 1 && FAST) {
     if (K <= 16) {
       float a1;
-      const float lp1 = grad1_packed(z[0], row, zh, zs, a.prog.types[0], K, a.P, a.trainable != 0, gl,
-                                     a.out != nullptr, a1);
+      const float lp1 = CM == kChainPairs ? grad1_pairs(z[0], row, zh, zs, a.prog.types[0], K, a.P,
+                                                        a.trainable != 0, gl, a.out != nullptr, a1)
+                                          : grad1_packed(z[0], row, zh, zs, a.prog.types[0], K, a.P,
+                                                         a.trainable != 0, gl, a.out != nullptr, a1);
       adj[0] = a1;
       return lp1;
     }

@@ -16,6 +16,18 @@ template <int Q>
 void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
   auto kfn = (kFast && a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? chain_wave1_kernel<kFast, Q, kFast>
                                                                         : chain_wave1_kernel<kFast, Q, false>;
+#if NFN_FAST
+  if (a.prog.K <= kPairsMaxKStream && env_int("NFN_PACKED", 1) == 1)
+    kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
+#ifdef NFN_DIAG
+  // chain-form A/B (diag build): 0 = loop, 3 = pairs, 2 = the C2 program at compile time
+  const int cm = env_int("NFN_CHAIN_FORM", -1);
+  if (cm == kChainLoop && a.prog.K <= 16) kfn = chain_wave1_kernel<true, Q, true>;
+  if (cm == kChainPairs && a.prog.K <= 16) kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
+  if (cm == kStaticProg && a.prog.K == kStaticK[0] && a.prog.types[0] == kStaticTypes[0])
+    kfn = chain_wave1_kernel<true, Q, true, false, kStaticProg>;
+#endif
+#endif
   const int64_t units = a.ntiles;
   const int teams = T / 64;
   // Resident workgroups per CU: a long chain (C2: 10 flows) keeps each wave busy
@@ -100,8 +112,15 @@ void launch_p_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream
 #if NFN_FAST
 template <int Q>
 void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
-  auto kfn = (a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? posterior_wave1_kernel<Q, true>
+  // two flows per dispatch (chain1_fast_pairs): C5 0.180 -> 0.169 ms, bitwise the same values
+  auto kfn = (a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? posterior_wave1_kernel<Q, true, kChainPairs>
                                                                 : posterior_wave1_kernel<Q, false>;
+#ifdef NFN_DIAG
+  const int cm = env_int("NFN_CHAIN_FORM", kChainPairs);
+  if (cm == kChainLoop && a.prog.K <= 16) kfn = posterior_wave1_kernel<Q, true>;
+  if (cm == kStaticProg && a.prog.K == kStaticK[0] && a.prog.types[0] == kStaticTypes[0])
+    kfn = posterior_wave1_kernel<Q, true, kStaticProg>;
+#endif
   const int64_t units = a.ntiles * a.nsplit;
   const int64_t grid = cap_grid(std::min<int64_t>((units + 3) / 4, (int64_t)cu_count() * posterior_wave1_wgs_per_cu()), a);
   *grid_out = grid;

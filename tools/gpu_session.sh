@@ -113,6 +113,13 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_sq2_dgrad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_sq2_dgrad" -o s2 -- \
         python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_sq_fwd)  # issue / stall breakdown of the C5 posterior and the C2 forward (two counter passes each)
+      for cfg in C5 C2; do
+        { cd /tmp; run pmc_sq1_$cfg 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d "$OUT/pmc_sq1_$cfg" -o s1 -- \
+          python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+        { cd /tmp; run pmc_sq2_$cfg 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_IFETCH SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_$cfg" -o s2 -- \
+          python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+      done ;;
     bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
     parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     sampleerr) run sampleerr 200 python tools/sample_err.py ;;
@@ -136,6 +143,11 @@ for s in $STEPS; do
     traintests) run traintests 400 python -u -m pytest tests/test_gpu_training.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep) run sweep 300 python tools/microbench.py sweep ;;
     slices) run slices 300 python tools/microbench.py slices ;;
+    chainform) run chainform 400 python tools/microbench.py chainform ;;
+    kthresh) run kthresh 400 python tools/microbench.py kthresh ;;
+    gradform) run gradform 400 python tools/microbench.py gradform ;;
+    dgradcmp) run dgradcmp 200 python tools/microbench.py dgradcmp ;;
+    chainform_dense) run chainform_dense 400 python tools/microbench.py chainform_dense ;;
     wstests) run wstests 400 python -u -m pytest tests/test_gpu_workspace.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     pcie) run pcie 300 python tools/microbench.py pcie ;;
     prio) run prio 300 python tools/microbench.py prio ;;

@@ -24,6 +24,10 @@ CFG = {
     "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22, None),
     "C5": (("planar", "radial") * 5, 1, 1 << 17, 64),
     "C1": (("radial", "radial"), 1, 1 << 24, None),
+    "K4": (("planar", "radial") * 2, 1, 1 << 24, None),
+    "K6": (("planar", "radial") * 3, 1, 1 << 24, None),
+    "K8": (("planar", "radial") * 4, 1, 1 << 24, None),
+    "R10": (("radial",) * 10, 1, 1 << 24, None),
 }
 
 
@@ -189,6 +193,14 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
         "unfused_gemm_plus_posterior": lambda: ops.posterior_lse(y, torch.matmul(h, W) + b[:, None], ft, d, True),
         "posterior_on_resident_t": lambda: ops.posterior_lse(y, t, ft, d, True),
     }
+
+    def loopform():
+        os.environ["NFN_CHAIN_FORM"] = "0"
+        r_ = ops.posterior_lse_dense(y, h, W, b, ft, d, True)
+        del os.environ["NFN_CHAIN_FORM"]
+        return r_
+
+    fns["fused_loopform"] = loopform
     stream = torch.cuda.current_stream()
     prewarm(fns["fused"])
     times = {k: [] for k in fns}
@@ -239,10 +251,20 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
         "fused": fused,
         "fused_generic": fused,
         "fused_gemms_only": fused,
+        "fused_loopform": fused,
         "unfused": unfused,
         "chain_backward_on_resident_t": lambda: ops.chain_log_prob_grad(y, t, ft, d, True, g_out=g),
     }
-    envs = {"fused_generic": {"NFN_DENSE1_GRAD": "0"}, "fused_gemms_only": {"NFN_ABLATE_FLOWS": "1"}}
+    envs = {"fused_generic": {"NFN_DENSE1_GRAD": "0"}, "fused_gemms_only": {"NFN_ABLATE_FLOWS": "1"},
+            "fused_loopform": {"NFN_CHAIN_FORM": "0"}}
+    os.environ["NFN_CHAIN_FORM"] = "0"
+    loop_out = [x for x in fused()]
+    del os.environ["NFN_CHAIN_FORM"]
+    for name, a_, b_ in zip(("lp", "dh", "dW", "db", "dy"), [x for x in fused()], loop_out):
+        if a_ is None:
+            continue
+        print(json.dumps({"check": "pairs vs loop chain form", "what": name,
+                          "max_abs": float((a_ - b_).abs().max().item())}), flush=True)
     ref = [x for x in fused()[1:]]
     os.environ["NFN_DENSE1_GRAD"] = "0"
     gen_out = [x for x in fused()[1:]]
@@ -464,6 +486,62 @@ def main():
             m = float(np.median(ms))
             print(json.dumps({"variant": name, "ms": m, "GBps": nbytes / m / 1e6, "frac8TBs": nbytes / m / 1e6 / 8000}),
                   flush=True)
+        return
+    if which[0] == "kthresh":  # chain length at which the pair form stops paying in the streaming kernels
+        for cfg in ("K4", "K6", "K8", "R10"):
+            run(cfg, [{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}}], rounds=2)
+            run_grad(cfg, [{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}}],
+                     reps=10, rounds=2)
+        return
+    if which[0] == "gradform":  # pair form in the plain fused backward (C2, C1)
+        for cfg in ("C2", "C1"):
+            run_grad(cfg, [{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}},
+                           {"name": "loop_compute", "env": {"NFN_ABLATE_LOADS": 1}},
+                           {"name": "pairs_compute", "env": {"NFN_CHAIN_FORM": 3, "NFN_ABLATE_LOADS": 1}}],
+                     reps=10, rounds=2)
+        run(cfg="C1", variants=[{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}}])
+        return
+    if which[0] == "dgradcmp":  # pair vs loop chain form in the fused Dense backward: where do dh / dW differ
+        ft, d, H = ("planar", "radial") * 5, 1, 16
+        P = ops.total_param_size(ft, d, True)
+        for B in (4096, 1 << 20):
+            gen = torch.Generator(device="cuda").manual_seed(5)
+            y = torch.randn((B, d), generator=gen, device="cuda")
+            h = torch.randn((B, H), generator=gen, device="cuda")
+            W = torch.randn((H, P), generator=gen, device="cuda") / 4.0
+            b = 0.1 * torch.randn((P,), generator=gen, device="cuda")
+            g = torch.full((B,), -1.0 / B, device="cuda")
+            outs = {}
+            for form in ("3", "0"):
+                os.environ["NFN_CHAIN_FORM"] = form
+                outs[form] = ops.chain_log_prob_dense_grad(y, h, W, b, ft, d, True, g_out=g)
+                del os.environ["NFN_CHAIN_FORM"]
+            (_, dh3, dW3, db3, dy3), (_, dh0, dW0, db0, dy0) = outs["3"], outs["0"]
+            rowdiff = (dh3 - dh0).abs().amax(1)
+            bad = torch.nonzero(rowdiff > 0).flatten()
+            print(json.dumps({"B": B, "dh_rows_differing": int(bad.numel()),
+                              "dh_max_abs": float(rowdiff.max().item()),
+                              "dh_max_rel_row": float((rowdiff / (dh0.abs().amax(1) + 1e-30)).max().item()),
+                              "first_bad_rows": bad[:8].tolist(),
+                              "dW_max_rel": float(((dW3 - dW0).abs() / (dW0.abs() + 1e-30)).max().item()),
+                              "db_equal": bool(torch.equal(db3, db0)), "dy_equal": bool(torch.equal(dy3, dy0))}),
+                  flush=True)
+        return
+    if which[0] == "chainform_dense":  # the pair form in the fused Dense kernels
+        run_dense([{"name": "dense1_pairs", "env": {}}, {"name": "dense1_loop", "env": {"NFN_CHAIN_FORM": 0}}])
+        run_posterior_dense()
+        run_dense_grad()
+        return
+    if which[0] == "chainform":  # d = 1 chain as a packed loop, two flows per dispatch, or a compile-time program
+        forms = [("loop", 0), ("pairs", 3), ("static", 2)]
+        for cfg in ("C2", "C5"):
+            v = []
+            for name, cm in forms:
+                v.append({"name": name, "env": {"NFN_CHAIN_FORM": cm}})
+                v.append({"name": name + "_compute", "env": {"NFN_CHAIN_FORM": cm, "NFN_ABLATE_LOADS": 1}})
+                for wg in (3, 4):
+                    v.append({"name": f"{name}_wg{wg}", "env": {"NFN_CHAIN_FORM": cm, "NFN_WG_PER_CU": wg}})
+            run(cfg, v, reps=20, rounds=2)
         return
     if which[0] == "dense":  # fused Dense -> chain: wave1-style pipeline vs generic, occupancy
         run_dense([{"name": "dense1", "env": {}}, {"name": "generic", "env": {"NFN_DENSE1": 0}},
