@@ -1,0 +1,86 @@
+"""The d = 1 chain two flows per dispatch (`chain1_fast_pairs` / `grad1_pairs`,
+DESIGN.md "The d = 1 chain is instruction-issue-bound").
+
+The pair form runs in the posterior, the fused Dense kernels and, for chains of at most
+4 flows, the streaming forward / backward. These programs reach those kernels (rows of
+P = 8, 16 or 32 floats: P/4 a power of two), with odd and even flow counts, affine
+blocks of 2 parameters between the 3-parameter ones, and the longest packed chains.
+Forward, posterior and backward are held to the oracles at the tolerances the other GPU
+tests use: `tolerance_bound` for log-densities and `grad_tolerance` for gradients."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nfn_grad_oracle as G
+from oracle import nfn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+PROGRAMS = [
+    ("affine",) * 3,                                              # K = 3, P = 8
+    ("radial", "radial"),                                         # K = 2, P = 8 (C1)
+    ("planar", "affine", "radial"),                               # K = 3, P = 10: generic kernels
+    ("planar", "radial", "planar", "affine", "radial"),           # K = 5, P = 16
+    ("planar", "affine", "radial", "affine", "affine", "affine"),  # K = 6, P = 16
+    ("affine",) * 15,                                             # K = 15, P = 32
+    ("radial", "planar") * 5,                                     # K = 10, P = 32
+]
+
+
+def _ids(ft):
+    return "-".join(f[0] for f in ft)
+
+
+@pytest.mark.parametrize("ft", PROGRAMS, ids=_ids)
+def test_pair_form_forward_and_posterior(ft, gpu):
+    from normalizingflownetwork_amd import ops
+
+    rng = np.random.default_rng(len(ft) * 31 + len(ft[0]))
+    P = O.total_param_size(ft, 1, True)
+    B = 1000
+    y = rng.standard_normal((B, 1)).astype(np.float32)
+    t = (0.7 * rng.standard_normal((B, P))).astype(np.float32)
+    lp, _ = ops.chain_log_prob(y, t, ft, 1, True)
+    with np.errstate(all="ignore"):
+        r64 = O.chain_log_prob(y, t, ft, 1, True, np.float64)
+        r32 = O.chain_log_prob(y, t, ft, 1, True, np.float32)
+    got = lp.cpu().numpy()
+    ok = np.isfinite(r64)
+    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    # posterior: S draws of t per sample
+    S, Bp = 3, 333
+    tp = (0.7 * rng.standard_normal((S, Bp, P))).astype(np.float32)
+    out, _ = ops.posterior_lse(y[:Bp], tp, ft, 1, True)
+    with np.errstate(all="ignore"):
+        p64 = O.posterior_lse(y[:Bp], tp, ft, 1, True)
+        p32 = O.posterior_lse(y[:Bp], tp, ft, 1, True, dtype=np.float32)
+    got = out.cpu().numpy()
+    ok = np.isfinite(p64)
+    assert (np.abs(got[ok] - p64[ok]) <= O.tolerance_bound(p64[ok], p32[ok])).all()
+
+
+@pytest.mark.parametrize("ft", [p for p in PROGRAMS if len(p) <= 6], ids=_ids)
+def test_pair_form_backward(ft, gpu):
+    from normalizingflownetwork_amd import ops
+
+    rng = np.random.default_rng(7 * len(ft))
+    P = O.total_param_size(ft, 1, True)
+    B = 64 * 5 + 17
+    y = rng.standard_normal((B, 1)).astype(np.float32)
+    t = (0.7 * rng.standard_normal((B, P))).astype(np.float32)
+    g = rng.standard_normal(B).astype(np.float32)
+    gt64, gy64, dev_t, dev_y = G.fp32_spread(y, t, ft, 1, True, g_out=g)
+    lp, gt, gy = ops.chain_log_prob_grad(torch.from_numpy(y).to(gpu), torch.from_numpy(t).to(gpu), ft, 1, True,
+                                         g_out=torch.from_numpy(g).to(gpu), want_logp=True)
+    for got, ref, dev, what in ((gt, gt64, dev_t, "d/dt"), (gy, gy64, dev_y, "d/dy")):
+        got = got.cpu().numpy().astype(np.float64).reshape(ref.shape)
+        fin = np.isfinite(ref)
+        assert np.array_equal(np.isfinite(got), fin), what
+        assert (np.abs(got[fin] - ref[fin]) <= G.grad_tolerance(ref, dev)[fin]).all(), what
+    with np.errstate(all="ignore"):
+        r64 = O.chain_log_prob(y, t, ft, 1, True, np.float64)
+        r32 = O.chain_log_prob(y, t, ft, 1, True, np.float32)
+    got = lp.cpu().numpy()
+    ok = np.isfinite(r64)
+    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()

@@ -121,6 +121,7 @@ for s in $STEPS; do
           python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       done ;;
     bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
+    pairtests) run pairtests 300 python -u -m pytest tests/test_gpu_pairs.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     sampleerr) run sampleerr 200 python tools/sample_err.py ;;
     sampletests) run sampletests 300 python -u -m pytest tests/test_gpu_sample.py tests/test_gpu_training.py -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
