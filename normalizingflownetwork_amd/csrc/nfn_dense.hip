@@ -583,6 +583,9 @@ void launch_d1(const DenseArgs& da, size_t /*generic kernel's LDS*/, hipStream_t
                      : (nn == 2 ? chain_dense1_kernel<QH, 2, CM> : (nn == 3 ? chain_dense1_kernel<QH, 3, CM>
                                                                            : chain_dense1_kernel<QH, 4, CM>));
 #ifdef NFN_DIAG
+  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kStaticProg && nn == 2 && da.c.prog.K == kStaticK[0] &&
+      da.c.prog.types[0] == kStaticTypes[0])
+    kfn = chain_dense1_kernel<QH, 2, kStaticProg>;
   if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop)
     kfn = nn <= 1 ? chain_dense1_kernel<QH, 1>
                   : (nn == 2 ? chain_dense1_kernel<QH, 2> : (nn == 3 ? chain_dense1_kernel<QH, 3>

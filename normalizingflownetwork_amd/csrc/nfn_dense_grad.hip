@@ -381,7 +381,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
     // 3. the chain forward + reverse per lane: the t column entries become g * d logp / d t
     float adj, z = z0;
     float lp;
-    if constexpr (CM == kChainPairs)
+    if constexpr (CM == kStaticProg)
+      lp = grad1_static<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, zh, 64, P, trainable, gl, a.out != nullptr,
+                                                           adj) - corr;
+    else if constexpr (CM == kChainPairs)
       lp = grad1_pairs<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
     else
       lp = grad1_packed<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
@@ -497,6 +500,11 @@ int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
   auto kfn = chain_dense1_grad_kernel<MH, NN, kChainPairs>;
 #ifdef NFN_DIAG
   if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop) kfn = chain_dense1_grad_kernel<MH, NN>;
+  if constexpr (NN == 2) {
+    if (env_int("NFN_CHAIN_FORM", kChainPairs) == kStaticProg && g.da.c.prog.K == kStaticK[0] &&
+        g.da.c.prog.types[0] == kStaticTypes[0])
+      kfn = chain_dense1_grad_kernel<MH, NN, kStaticProg>;
+  }
 #endif
   const size_t lds = (size_t)4 * dense1_grad_wave_floats(g.da.c.P, 16 * MH + 4, g.da.c.prog.K) * sizeof(float);
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);

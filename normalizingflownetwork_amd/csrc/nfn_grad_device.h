@@ -505,6 +505,55 @@ __device__ __forceinline__ float grad1_pairs(float& z, float* row, float* zh, in
 }
 
 
+// Diagnostic experiment: grad1_packed for one program fixed at compile time (flow
+// inputs in registers, straight-line code).
+template <uint32_t TYPES, int K, int ST = 1>
+__device__ __forceinline__ float grad1_static(float& z, float* row, float* zh, int zs, int P, bool trainable,
+                                              float gl, bool want_lp, float& adj) {
+  (void)zh;
+  (void)zs;
+  float l2 = 0.0f;
+  float zk[K];
+  int off = P;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int id = (int)((TYPES >> (2 * k)) & 3u);
+    off -= size1(id);
+    float pc[3];
+    read3c<ST>(pc, row, off);
+    zk[k] = z;
+    if (want_lp)
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+    else
+      flow1_z(id, z, pc);
+  }
+  const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  float a1;
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[ST], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    a1 = -gz;
+    row[0] = gz;
+    row[ST] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+  } else {
+    a1 = -gl * z;
+  }
+  int ob = trainable ? 2 : 0;
+#pragma unroll
+  for (int k = K - 1; k >= 0; --k) {
+    const int id = (int)((TYPES >> (2 * k)) & 3u);
+    float pc[3];
+    read3c<ST>(pc, row, ob);
+    flow1_bwd<ST>(id, zk[k], a1, pc, row + ob * ST, gl);
+    ob += size1(id);
+  }
+  adj = a1;
+  return lp;
+}
+
 // ---------------------------------------------------------------------------
 // Lane-group forms (d >= 4): a G-lane group owns one sample, lane j holds the
 // DPL dimensions j, j + G, ...; inner products are DPP group sums (gsum).

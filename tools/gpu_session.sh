@@ -147,6 +147,7 @@ for s in $STEPS; do
     chainform) run chainform 400 python tools/microbench.py chainform ;;
     kthresh) run kthresh 400 python tools/microbench.py kthresh ;;
     gradform) run gradform 400 python tools/microbench.py gradform ;;
+    staticdense) run staticdense 300 python tools/microbench.py staticdense ;;
     dgradcmp) run dgradcmp 200 python tools/microbench.py dgradcmp ;;
     chainform_dense) run chainform_dense 400 python tools/microbench.py chainform_dense ;;
     wstests) run wstests 400 python -u -m pytest tests/test_gpu_workspace.py -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;

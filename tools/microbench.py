@@ -227,7 +227,7 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
                           "rounds_ms": times[k]}), flush=True)
 
 
-def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
+def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False):
     """C2 training step through the output Dense layer: the fused backward (t never
     written) vs the unfused path (library GEMM t, chain backward kernel, GEMMs for
     dh / dW and the db sum) vs the chain backward alone on a resident t."""
@@ -257,6 +257,9 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3):
     }
     envs = {"fused_generic": {"NFN_DENSE1_GRAD": "0"}, "fused_gemms_only": {"NFN_ABLATE_FLOWS": "1"},
             "fused_loopform": {"NFN_CHAIN_FORM": "0"}}
+    if static:
+        fns = {"fused": fused, "fused_static": fused, "fused_loopform": fused}
+        envs["fused_static"] = {"NFN_CHAIN_FORM": "2"}
     os.environ["NFN_CHAIN_FORM"] = "0"
     loop_out = [x for x in fused()]
     del os.environ["NFN_CHAIN_FORM"]
@@ -526,6 +529,10 @@ def main():
                               "dW_max_rel": float(((dW3 - dW0).abs() / (dW0.abs() + 1e-30)).max().item()),
                               "db_equal": bool(torch.equal(db3, db0)), "dy_equal": bool(torch.equal(dy3, dy0))}),
                   flush=True)
+        return
+    if which[0] == "staticdense":  # how much a compile-time program would add in the fused Dense kernels
+        run_dense([{"name": "dense1_pairs", "env": {}}, {"name": "dense1_static", "env": {"NFN_CHAIN_FORM": 2}}])
+        run_dense_grad(static=True)
         return
     if which[0] == "chainform_dense":  # the pair form in the fused Dense kernels
         run_dense([{"name": "dense1_pairs", "env": {}}, {"name": "dense1_loop", "env": {"NFN_CHAIN_FORM": 0}}])
