@@ -84,3 +84,25 @@ def test_pair_form_backward(ft, gpu):
     got = lp.cpu().numpy()
     ok = np.isfinite(r64)
     assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+
+
+@pytest.mark.parametrize("ft", [("planar", "radial") * 5, ("affine",) * 15, ("planar", "radial", "planar", "affine", "radial")],
+                         ids=_ids)
+def test_pair_form_bitwise_the_loop(ft, gpu):
+    """At K > 4 the streaming forward keeps the one-flow loop while the posterior runs the
+    pair form; with one draw the posterior's log-sum-exp is the log-density itself
+    (m + log 1 - log 1), so the two kernels must agree bit for bit."""
+    from normalizingflownetwork_amd import ops
+
+    prev = ops.set_math_mode("fast")
+    try:
+        gen = torch.Generator(device="cuda").manual_seed(len(ft))
+        P = O.total_param_size(ft, 1, True)
+        B = 64 * 70 + 9
+        y = torch.randn((B, 1), generator=gen, device="cuda")
+        t = 0.7 * torch.randn((B, P), generator=gen, device="cuda")
+        lp, _ = ops.chain_log_prob(y, t, ft, 1, True)
+        post, _ = ops.posterior_lse(y, t.unsqueeze(0).contiguous(), ft, 1, True)
+        assert torch.equal(lp, post)
+    finally:
+        ops.set_math_mode(prev)
