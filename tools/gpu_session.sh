@@ -154,6 +154,7 @@ for s in $STEPS; do
     pcie) run pcie 300 python tools/microbench.py pcie ;;
     prio) run prio 300 python tools/microbench.py prio ;;
     ceiling) run ceiling 200 python tools/microbench.py ceiling ;;
+    copyceil) run copyceil 120 ./tools/copy_ceiling ;;
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
     gradc3) run gradc3 300 python tools/microbench.py gradc3 ;;
     gradc3z) run gradc3z 300 python tools/microbench.py gradc3z ;;
