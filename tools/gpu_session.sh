@@ -158,6 +158,7 @@ for s in $STEPS; do
     gradmicro) run gradmicro 400 python tools/microbench.py grad ;;
     gradc3) run gradc3 300 python tools/microbench.py gradc3 ;;
     gradc3z) run gradc3z 300 python tools/microbench.py gradc3z ;;
+    gradc3tape) run gradc3tape 300 python tools/microbench.py gradc3tape ;;
     *) echo "unknown step $s" ;;
   esac
 done

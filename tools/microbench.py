@@ -581,6 +581,13 @@ def main():
                         {"name": "with_ldj_compute_only", "env": {"NFN_GRAD_ZONLY": 0, "NFN_ABLATE_LOADS": 1}},
                         {"name": "zonly_b", "env": {}}, {"name": "with_ldj_b", "env": {"NFN_GRAD_ZONLY": 0}}])
         return
+    if which[0] == "gradc3tape":  # C3 backward: per-flow scalars taped in LDS vs recomputed in the reverse pass
+        run_grad("C3", [{"name": "tape", "env": {}}, {"name": "recompute", "env": {"NFN_GRAD_TAPE": 0}},
+                        {"name": "tape_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+                        {"name": "recompute_compute_only", "env": {"NFN_GRAD_TAPE": 0, "NFN_ABLATE_LOADS": 1}},
+                        {"name": "tape_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                        {"name": "tape_b", "env": {}}, {"name": "recompute_b", "env": {"NFN_GRAD_TAPE": 0}}])
+        return
     if which[0] == "grad":
         v = [{"name": "wave", "env": {}},
              {"name": "wpb4", "env": {"NFN_GRAD_WPB": 4}},
