@@ -256,6 +256,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
   float* zh = tl + R * S + lane;
   float* pad = lds + nwave * slot + 4 * lane;
   const int nslots = R * Q;
+  // the tile's float4 slots: S, the slot size and the pad are multiples of 4 floats and
+  // the dynamic LDS starts at 0 (no static LDS), so every slot is 16-byte aligned.
+  // Indexing a float4 view (not a float pointer at a runtime offset) lets the compiler
+  // emit ds_write_b128 / ds_read_b128; the split ds_*2_b32 pairs it emits otherwise put
+  // lanes 16 B apart on the same banks (4-way conflicts: SQ_LDS_BANK_CONFLICT 1.1e8).
+  float4* lds4 = reinterpret_cast<float4*>(__builtin_assume_aligned(lds, 16));
   int loff[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -312,7 +318,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
     const int64_t nr = max((int64_t)0, min((int64_t)R, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
-    for (int k = 0; k < NV; ++k) *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
+    for (int k = 0; k < NV; ++k) lds4[loff[k] >> 2] = buf[k];
     float z[DPL];
 #pragma unroll
     for (int i = 0; i < DPL; ++i) z[i] = norm ? f_div<FAST>(ybuf[i] - ymean[i], ystd[i]) : ybuf[i];
@@ -412,7 +418,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
       const auto rgt = tile_rsrc(nr > 0 ? ga.grad_t + b0 * P : ga.grad_t, nr * P * 4);
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        const float4 t4 = *reinterpret_cast<const float4*>(lds + loff[k]);
+        const float4 t4 = lds4[loff[k] >> 2];
         __builtin_amdgcn_raw_buffer_store_b128(f32x4{t4.x, t4.y, t4.z, t4.w}, rgt, lane * 16, k * 1024, kNT);
       }
     }

@@ -120,6 +120,11 @@ for s in $STEPS; do
         { cd /tmp; run pmc_sq2_$cfg 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_IFETCH SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_$cfg" -o s2 -- \
           python3 "$ROOT/bench.py" --config $cfg --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       done ;;
+    pmc_sq_grad_c3)  # issue / stall breakdown of the C3 backward (two counter passes)
+      { cd /tmp; run pmc_sq1_grad_c3 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d "$OUT/pmc_sq1_grad_c3" -o s1 -- \
+        python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_sq2_grad_c3 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_grad_c3" -o s2 -- \
+        python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
     bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
     pairtests) run pairtests 300 python -u -m pytest tests/test_gpu_pairs.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
