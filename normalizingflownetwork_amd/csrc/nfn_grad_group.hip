@@ -40,6 +40,8 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
   const int Q = a.P >> 2;
   const int S = a.lds_stride;
   const bool lds4 = (S & 3) == 0;
+  // float4 view for the 16-byte-aligned slots (lds4): b128 LDS accesses, not ds_*2_b32 pairs
+  float4* const l4v = reinterpret_cast<float4*>(__builtin_assume_aligned(lds, 16));
   const int64_t rs = a.t_rowstride;
   const int64_t gts = ga.gt_rowstride;
   const int slot = R * S + K * DPL * 64;
@@ -100,7 +102,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
         if (lane + k * 64 < nslots && r < nr) {
           float* dst = tl + r * S + 4 * c;
           if (lds4) {
-            *reinterpret_cast<float4*>(dst) = buf[k];
+            l4v[(int)(dst - lds) >> 2] = buf[k];
           } else {
             dst[0] = buf[k].x;
             dst[1] = buf[k].y;
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
           const float* src = tl + r * S + 4 * c;
           f32x4 v;
           if (lds4) {
-            const float4 t4 = *reinterpret_cast<const float4*>(src);
+            const float4 t4 = l4v[(int)(src - lds) >> 2];
             v = f32x4{t4.x, t4.y, t4.z, t4.w};
           } else {
             v = f32x4{src[0], src[1], src[2], src[3]};

@@ -125,6 +125,13 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_sq2_grad_c3 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_grad_c3" -o s2 -- \
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_lds)  # LDS bank-conflict cycles of every bench kernel (one counter pass per mode)
+      i=0
+      for args in "--config C2" "--mode grad --config C2" "--config C3" "--config C5" "--mode dense_grad" "--mode dense" "--mode bijector"; do
+        i=$((i+1))
+        { cd /tmp; run pmc_lds_$i 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace --output-format csv -d "$OUT/pmc_lds_$i" -o l -- \
+          python3 "$ROOT/bench.py" $args --steps 3 --warmup 1 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+      done ;;
     bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
     pairtests) run pairtests 300 python -u -m pytest tests/test_gpu_pairs.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
