@@ -236,7 +236,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
 // y, g_out, log_prob and grad_y go through buffer instructions too, and nothing
 // branches between a load and its use (rows past B compute on zeros; their
 // stores fall outside the descriptors).
-template <int G, int DPL, bool FAST, int NV, bool FULL>
+// SPLIT (diagnostic build only): the tile's LDS accesses through float pointers at runtime
+// offsets, as before the float4 view (ds_*2_b32 pairs) — the A/B reference.
+template <int G, int DPL, bool FAST, int NV, bool FULL, bool SPLIT = false>
 __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs ga) {
   const ChainArgs& a = ga.c;
   extern __shared__ float lds[];
@@ -320,7 +322,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
     const int64_t nr = max((int64_t)0, min((int64_t)R, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
-    for (int k = 0; k < NV; ++k) lds4[loff[k] >> 2] = buf[k];
+    for (int k = 0; k < NV; ++k) {
+      if constexpr (SPLIT)
+        *reinterpret_cast<float4*>(lds + loff[k]) = buf[k];
+      else
+        lds4[loff[k] >> 2] = buf[k];
+    }
     float z[DPL];
 #pragma unroll
     for (int i = 0; i < DPL; ++i) z[i] = norm ? f_div<FAST>(ybuf[i] - ymean[i], ystd[i]) : ybuf[i];
@@ -420,7 +427,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
       const auto rgt = tile_rsrc(nr > 0 ? ga.grad_t + b0 * P : ga.grad_t, nr * P * 4);
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        const float4 t4 = lds4[loff[k] >> 2];
+        const float4 t4 = SPLIT ? *reinterpret_cast<const float4*>(lds + loff[k]) : lds4[loff[k] >> 2];
         __builtin_amdgcn_raw_buffer_store_b128(f32x4{t4.x, t4.y, t4.z, t4.w}, rgt, lane * 16, k * 1024, kNT);
       }
     }
@@ -432,6 +439,11 @@ template <int G, int DPL, int NV>
 void launch_gg1(const GradArgs& ga, hipStream_t s, int64_t* grid_out) {
   auto kfn = ga.c.d == G * DPL ? chain_grad_group1_kernel<G, DPL, kFast, NV, true>
                                 : chain_grad_group1_kernel<G, DPL, kFast, NV, false>;
+#ifdef NFN_DIAG
+  if (env_int("NFN_LDS_SPLIT", 0) == 1)
+    kfn = ga.c.d == G * DPL ? chain_grad_group1_kernel<G, DPL, kFast, NV, true, true>
+                            : chain_grad_group1_kernel<G, DPL, kFast, NV, false, true>;
+#endif
   const int wpb = env_int("NFN_GRAD_GROUP_WPB", 4) == 2 ? 2 : 4;
   const int R = 64 / G;
   const size_t lds_b = ((size_t)wpb * (R * ga.c.lds_stride + ga.c.prog.K * DPL * 64) + 64 * 4) * sizeof(float);

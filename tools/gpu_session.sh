@@ -171,6 +171,7 @@ for s in $STEPS; do
     gradc3) run gradc3 300 python tools/microbench.py gradc3 ;;
     gradc3z) run gradc3z 300 python tools/microbench.py gradc3z ;;
     gradc3tape) run gradc3tape 300 python tools/microbench.py gradc3tape ;;
+    gradc3b128) run gradc3b128 300 python tools/microbench.py gradc3b128 ;;
     *) echo "unknown step $s" ;;
   esac
 done

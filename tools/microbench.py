@@ -581,6 +581,13 @@ def main():
                         {"name": "with_ldj_compute_only", "env": {"NFN_GRAD_ZONLY": 0, "NFN_ABLATE_LOADS": 1}},
                         {"name": "zonly_b", "env": {}}, {"name": "with_ldj_b", "env": {"NFN_GRAD_ZONLY": 0}}])
         return
+    if which[0] == "gradc3b128":  # C3 backward: b128 LDS tile accesses vs the split ds_*2_b32 pairs
+        run_grad("C3", [{"name": "b128", "env": {}}, {"name": "split", "env": {"NFN_LDS_SPLIT": 1}},
+                        {"name": "b128_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+                        {"name": "split_compute_only", "env": {"NFN_LDS_SPLIT": 1, "NFN_ABLATE_LOADS": 1}},
+                        {"name": "b128_b", "env": {}}, {"name": "split_b", "env": {"NFN_LDS_SPLIT": 1}}],
+                 rounds=4)
+        return
     if which[0] == "gradc3tape":  # C3 backward: per-flow scalars taped in LDS vs recomputed in the reverse pass
         run_grad("C3", [{"name": "tape", "env": {}}, {"name": "recompute", "env": {"NFN_GRAD_TAPE": 0}},
                         {"name": "tape_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
