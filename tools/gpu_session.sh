@@ -172,6 +172,7 @@ for s in $STEPS; do
     gradc3z) run gradc3z 300 python tools/microbench.py gradc3z ;;
     gradc3tape) run gradc3tape 300 python tools/microbench.py gradc3tape ;;
     gradc3b128) run gradc3b128 300 python tools/microbench.py gradc3b128 ;;
+    c3mem) run c3mem 300 python tools/microbench.py c3mem ;;
     *) echo "unknown step $s" ;;
   esac
 done

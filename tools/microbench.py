@@ -588,6 +588,10 @@ def main():
                         {"name": "b128_b", "env": {}}, {"name": "split_b", "env": {"NFN_LDS_SPLIT": 1}}],
                  rounds=4)
         return
+    if which[0] == "c3mem":  # C3 forward: full vs compute-only vs memory-only (is the hand-off on the critical path?)
+        run("C3", [{"name": "full", "env": {}}, {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+                   {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}}, {"name": "full_b", "env": {}}], rounds=4)
+        return
     if which[0] == "gradc3tape":  # C3 backward: per-flow scalars taped in LDS vs recomputed in the reverse pass
         run_grad("C3", [{"name": "tape", "env": {}}, {"name": "recompute", "env": {"NFN_GRAD_TAPE": 0}},
                         {"name": "tape_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
