@@ -35,6 +35,14 @@ def bytes_per_launch(d, P, B, S):
     return B * (4 * d + 4 * P + 4) if S is None else B * (S * 4 * P + 4 * d + 4)
 
 
+def maxdiff(x, ref):
+    """max |x - ref| where the two differ; equal values (incl. equal infinities) and NaN in
+    both count as 0, a NaN in only one of them as inf."""
+    same = (x == ref) | (torch.isnan(x) & torch.isnan(ref))
+    d = torch.where(same, torch.zeros_like(x), (x - ref).abs())
+    return float(d.nan_to_num(nan=float("inf")).max().item())
+
+
 def prewarm(fn, ms=400.0):
     """Untimed launches for >= `ms` of device time (the clocks ramp over the first tens of ms)."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -86,7 +94,7 @@ def run(cfg, variants, reps=20, rounds=3):
     bpl = bytes_per_launch(d, P, B, S)
     for v in variants:
         ms = float(np.median(times[v["name"]]))
-        diff = float((outs[v["name"]] - ref).abs().max().item())
+        diff = maxdiff(outs[v["name"]], ref)
         res.append({"cfg": cfg, "variant": v["name"], "ms": ms, "GBps": bpl / ms / 1e6, "frac8TBs": bpl / ms / 1e6 / 8000,
                     "evals_per_s": B * (S or 1) / ms * 1e3, "maxdiff_vs_first": diff, "rounds_ms": times[v["name"]]})
         print(json.dumps(res[-1]), flush=True)
@@ -129,7 +137,7 @@ def run_grad(cfg, variants, reps=10, rounds=3):
     bpl = B * (8 * d + 8 * P + 4)
     for v in variants:
         ms = float(np.median(times[v["name"]]))
-        diff = float((outs[v["name"]] - ref).abs().max().item())
+        diff = maxdiff(outs[v["name"]], ref)
         print(json.dumps({"cfg": cfg, "mode": "grad", "variant": v["name"], "ms": ms, "GBps": bpl / ms / 1e6,
                           "frac8TBs": bpl / ms / 1e6 / 8000, "maxdiff_vs_first": diff,
                           "rounds_ms": times[v["name"]]}), flush=True)
