@@ -95,7 +95,12 @@ extern "C" {
 
 #define NFN_COMM_ID_BYTES 128
 
-/* Library version as MAJOR*10000 + MINOR*100 + PATCH. */
+/* Library version as MAJOR*10000 + MINOR*100 + PATCH.
+ *   200 (0.2.0): out_sum is a device double[2] {sum, non-finite count} (was double[1]);
+ *                the workspace needs no initialisation (its finishing ticket is cleared on
+ *                the stream by every summed call).
+ *   100 (0.1.0): first release. */
+#define NFN_ABI_VERSION 200
 int32_t nfn_version(void);
 
 /* Message of the last failing call on this thread ("" if none). */
@@ -131,9 +136,10 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *                non-finite out_logp values}, finished inside the kernel by its last
  *                workgroup (fixed summation order: bitwise deterministic; no extra launch)
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
- *                ZERO-INITIALISED before its first use; every call leaves it reusable.
+ *                Needs no initialisation (e.g. a plain hipMalloc): a summed call clears
+ *                the ticket with a 4-byte stream-ordered memset before its launch.
  *                Layout: workspace[0] = number n of per-workgroup pairs written,
- *                workspace[1] = the finishing ticket (0 between calls), workspace[2 + 2i] /
+ *                workspace[1] = the finishing ticket, workspace[2 + 2i] /
  *                workspace[3 + 2i] = workgroup i's fp64 partial sum / non-finite count.
  *                With out_sum == NULL and workspace != NULL only the pairs are written
  *                (finish with nfn_reduce_partials_f64).  One workspace per call in

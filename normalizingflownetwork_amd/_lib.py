@@ -92,6 +92,9 @@ NFN_E_NULLPTR = -3
 NFN_E_HIP = -4
 NFN_E_COMM = -5
 NFN_COMM_ID_BYTES = 128
+# include/nfn.h NFN_ABI_VERSION: the binding's argument conventions (out_sum double[2],
+# uninitialised workspaces) hold for this version only
+ABI_VERSION = 200
 
 _lib = None
 
@@ -111,6 +114,9 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.nfn_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_NAME} has ABI version {lib.nfn_version()}, this binding needs {ABI_VERSION}; "
+                           "rebuild with `python -m normalizingflownetwork_amd.build --force`")
     _lib = lib
     return lib
 

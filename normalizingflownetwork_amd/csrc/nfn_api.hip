@@ -5,7 +5,7 @@
 
 #include "nfn_launch.h"
 
-#define NFN_VERSION_NUM 100  // 0.1.0
+#define NFN_VERSION_NUM NFN_ABI_VERSION  // include/nfn.h: the version history
 
 namespace nfn {
 
@@ -181,6 +181,33 @@ int32_t check_hip(const char* what) {
   return NFN_OK;
 }
 
+// The in-kernel finish counts workgroups on a ticket at workspace[1]; it is cleared on the
+// stream before every summed launch (a 4-byte memset node, graph-capturable), so the
+// workspace needs no initialisation and a call aborted mid-way cannot poison the next.
+int32_t reset_ticket(double* workspace, hipStream_t s) {
+  if (hipMemsetAsync(workspace + 1, 0, sizeof(uint32_t), s) != hipSuccess) return check_hip("hipMemsetAsync (ticket)");
+  return NFN_OK;
+}
+
+// Every argument check of the plain chain / posterior entry points that does not depend
+// on the launch shape: run before the first launch, so a rejected call has no side
+// effect on the stream (also when a long batch runs as several chunk launches).
+int32_t check_chain_args(const float* y, int64_t y_bstride, const float* t, int64_t t_drawstride,
+                         int64_t t_rowstride, int32_t S, int64_t B, int32_t d, int32_t P, const float* y_mean,
+                         const float* y_std, double* out_sum, double* workspace, bool posterior) {
+  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
+  if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
+  if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
+  if (posterior && S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
+  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  if (B == 0) return NFN_OK;
+  if (!y) return fail(NFN_E_NULLPTR, "y is NULL");
+  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
+  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
+  return NFN_OK;
+}
+
 // One launch over B samples.  A chunk of a longer batch (chunk_cap > 0) writes its
 // partial pairs after the earlier chunks' (from slot pair_base, at most chunk_cap of
 // them); only the last chunk finishes out_sum, over every chunk's pairs.
@@ -200,12 +227,11 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
   a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // measured +1-2% (C2, C5); 2 = + static split
-  if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
-  if (y_bstride < 0 || t_rowstride < 0 || t_drawstride < 0) return fail(NFN_E_SHAPE, "strides must be >= 0");
-  if (y_bstride != 0 && y_bstride < d) return fail(NFN_E_SHAPE, "y batch stride < n_dims");
-  if (t_rowstride != 0 && t_rowstride < P) return fail(NFN_E_SHAPE, "t row stride < total param size");
-  if (posterior && S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
-  if ((y_mean == nullptr) != (y_std == nullptr)) return fail(NFN_E_NULLPTR, "y_mean and y_std must both be given or both NULL");
+  {
+    const int32_t rc = check_chain_args(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, P, y_mean, y_std, out_sum,
+                                        workspace, posterior);
+    if (rc != NFN_OK) return rc;
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (B == 0) {
     if (out_sum) {
@@ -213,10 +239,11 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
     }
     return NFN_OK;
   }
-  if (!y) return fail(NFN_E_NULLPTR, "y is NULL");
-  if (P > 0 && !t) return fail(NFN_E_NULLPTR, "t is NULL");
-  if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
   if (!out && !workspace) return NFN_OK;
+  if (out_sum) {
+    const int32_t rc = reset_ticket(workspace, s);
+    if (rc != NFN_OK) return rc;
+  }
   const TileGeom g = tile_geom(P);
   a.y = y;
   a.t = t;
@@ -339,6 +366,11 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
                             y_std, out, out_sum, workspace, stream, posterior, 0, 0, nullptr);
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, nullptr);
   if (P < 0) return P;
+  {
+    const int32_t rc = check_chain_args(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, P, y_mean, y_std, out_sum,
+                                        workspace, posterior);
+    if (rc != NFN_OK) return rc;
+  }
   int64_t base = 0;
   for (int64_t b0 = 0; b0 < B; b0 += chunk) {
     const int64_t nb = std::min(chunk, B - b0);
@@ -475,6 +507,10 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   if ((reinterpret_cast<uintptr_t>(h) & 15) != 0) return fail(NFN_E_SHAPE, "h must be 16-byte aligned");
   if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
   if (!out && !workspace) return NFN_OK;
+  if (out_sum) {
+    const int32_t rc = reset_ticket(workspace, s);
+    if (rc != NFN_OK) return rc;
+  }
   a.y = y;
   a.y_mean = y_mean;
   a.y_std = y_std;
@@ -538,6 +574,10 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   if ((reinterpret_cast<uintptr_t>(h) & 15) != 0) return fail(NFN_E_SHAPE, "h must be 16-byte aligned");
   if (out_sum && !workspace) return fail(NFN_E_NULLPTR, "workspace is NULL but out_sum requested");
   if (!out && !workspace) return NFN_OK;
+  if (out_sum) {
+    const int32_t rc = reset_ticket(workspace, s);
+    if (rc != NFN_OK) return rc;
+  }
   a.y = y;
   a.y_mean = y_mean;
   a.y_std = y_std;

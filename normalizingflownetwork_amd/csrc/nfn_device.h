@@ -39,6 +39,12 @@
 
 #include "nfn.h"
 
+// The memory-pipeline details (buffer descriptors, counted vmcnt waits, the agent-scope
+// partial sums across the XCDs' L2s) are validated on gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "the nfn kernels are written for gfx950 (MI355X) only"
+#endif
+
 namespace nfn {
 
 constexpr int kMaxBlock = 256;
@@ -299,21 +305,29 @@ __device__ __forceinline__ float planar_step(float (&z)[DM], PTR p, int d) {
     }
   }
   const float b = p[2 * d];
-  const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
+  // softplus with RELATIVE accuracy as w.u -> -inf: it is the leading term of
+  // w.u_hat + 1 below once the constraint is active
+  const float sp = softplus_alpha<FAST>(wtu);
+  const float m_wtu = (-1.0f + sp) + 1e-5f;
   const float norm_w2 = nw2 + 1e-9f;
   const float coef = m_wtu - wtu;
   const float th = f_tanh<FAST>(wz + b);
   const float dth = 1.0f - th * th;
-  float s = 0.0f;
 #pragma unroll
   for (int j = 0; j < DM; ++j) {
     if (j < d) {
-      const float uh = u[j] + coef * f_div_acc<FAST>(w[j], norm_w2);
+      // d = 1: u + (m - wu) w / (w^2 + 1e-9) = (1e-9 u + m w) / (w^2 + 1e-9) exactly, with
+      // no cancellation between u and the correction as the constraint binds (w u -> -inf)
+      const float uh = d == 1 ? f_div_acc<FAST>(fmaf(u[j], 1e-9f, m_wtu * w[j]), norm_w2)
+                              : u[j] + coef * f_div_acc<FAST>(w[j], norm_w2);
       z[j] = z[j] + uh * th;
-      s += uh * (dth * w[j]);
     }
   }
-  return f_log<FAST>(fabsf(1.0f + s));
+  // 1 + (1 - th^2) w.u_hat with w.u_hat = m - coef 1e-9 / |w|^2 (PlanarFlow.py:49-53):
+  // th^2 + (1 - th^2)(softplus(w.u) + 1e-5 - coef 1e-9 / |w|^2), a sum of non-negative
+  // terms, where the reference's 1 + sum(u_hat psi) cancels as w.u_hat -> -1
+  const float qd = fmaf(-coef * 1e-9f, f_div<FAST>(1.0f, norm_w2), sp + 1e-5f);
+  return f_log<FAST>(fabsf(fmaf(th, th, dth * qd)));
 }
 
 // RadialFlow.py:24-33 (alpha, beta constraints), _r :45 (L1 norm), _h :48,
@@ -437,19 +451,31 @@ __device__ __forceinline__ float sp_fast1(float x) { return softplus_tf<true>(x)
 
 // The d = 1 bijectors return their Jacobian determinant (the caller accumulates
 // log2|det|); algebra is rearranged for fewer VALU issues, never for less accuracy.
-// Planar (PlanarFlow.py:23-33, :49-53, :72, :78-80):
-//   coef = (-1 + softplus(wtu) + 1e-5) - wtu,  u_hat = u + coef * w / (w^2 + 1e-9)
+// Planar (PlanarFlow.py:23-33, :49-53, :72, :78-80), in forms that stay well
+// conditioned where the reference's own fp32 order cancels (w u_hat -> -1):
+//   m = -1 + softplus(wu) + 1e-5 (softplus relative-accurate as wu -> -inf),
+//   u_hat = u + (m - wu) w / (w^2 + 1e-9) = (1e-9 u + m w) / (w^2 + 1e-9),
+//   det = 1 + (1 - th^2) w u_hat = th^2 + (1 - th^2)(softplus(wu) + 1e-5 - (m - wu) 1e-9 / (w^2 + 1e-9)),
 //   tanh(x) = 1 - 2 / (1 + e^{2x})
+__device__ __forceinline__ float planar1_uh(float u, float w, float nw2, float rn, float m) {
+  const float num = fmaf(u, 1e-9f, m * w);
+  const float q0 = num * rn;
+  return fmaf(fmaf(-nw2, q0, num), rn, q0);  // num / nw2, Newton-refined
+}
+
 __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, float b) {
   const float w = wraw + 1.0f;
   const float wtu = w * u;
   const float nw2 = fmaf(w, w, 1e-9f);
-  const float coef = sp_fast1(wtu) - (wtu + (1.0f - 1e-5f));
-  const float uh = fmaf(coef, f_div_acc<true>(w, nw2), u);
+  const float rn = __builtin_amdgcn_rcpf(nw2);
+  const float sp = softplus_alpha<true>(wtu);
+  const float m = sp - (1.0f - 1e-5f);
+  const float uh = planar1_uh(u, w, nw2, rn, m);
+  const float qd = fmaf((wtu - m) * 1e-9f, rn, sp + 1e-5f);
   const float E = __builtin_amdgcn_exp2f(fmaf(w, z, b) * (2.0f * kLog2e));
   const float th = 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));
   z = fmaf(uh, th, z);
-  return fmaf(uh, fmaf(-th, th, 1.0f) * w, 1.0f);
+  return fmaf(th, th, fmaf(-th, th, 1.0f) * qd);
 }
 
 // Radial (RadialFlow.py:24-33, :45-70) at d = 1: beta = softplus(.) - 1, so
@@ -826,6 +852,9 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
   const bool last = flag[0] != 0;
   __syncthreads();
   if (!last) return;
+  // Only the winning workgroup acquires (agent scope): the other workgroups' pairs,
+  // stored before their ticket increments, are visible to its loads below.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   sum_pairs<true>(partials, base + gridDim.x, red, out_sum);
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1456,33 +1485,35 @@ __device__ __forceinline__ float planar_gd(float (&z)[DPL], const float* p, int 
   const float wtu = gsum<G>(swu);
   const float nw2 = gsum<G>(sww);
   const float wz = gsum<G>(swz);
+  // The det is th^2 + (1 - th^2)(softplus(w.u) + 1e-5 - coef 1e-9 / |w|^2) (planar_step):
+  // no group sum of u_hat . w, and no cancellation as w.u_hat -> -1.
   if constexpr (FAST) {
-    // u_hat_i = u_i + (coef / |w|^2) w_i; dth factored out of the det sum.
-    const float c2 = f_div_acc<true>(softplus_tf<true>(wtu) - (wtu + (1.0f - 1e-5f)), nw2 + 1e-9f);
+    // u_hat_i = u_i + (coef / |w|^2) w_i
+    const float sp = softplus_alpha<true>(wtu);
+    const float c2 = f_div_acc<true>(sp - (wtu + (1.0f - 1e-5f)), nw2 + 1e-9f);
     const float th = f_tanh<true>(wz + b);
-    float sd = 0.0f;
 #pragma unroll
     for (int i = 0; i < DPL; ++i) {
       const float uh = fmaf(c2, w[i], u[i]);  // 0 on inactive dims
       z[i] = fmaf(uh, th, z[i]);
-      if constexpr (LDJ) sd = fmaf(uh, w[i], sd);
     }
     if constexpr (!LDJ) return 0.0f;
-    return f_log<true>(fabsf(fmaf(fmaf(-th, th, 1.0f), gsum<G>(sd), 1.0f)));
+    const float qd = fmaf(-c2, 1e-9f, sp + 1e-5f);
+    return f_log<true>(fabsf(fmaf(th, th, fmaf(-th, th, 1.0f) * qd)));
   }
-  const float m_wtu = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;
+  const float sp = softplus_alpha<FAST>(wtu);
+  const float m_wtu = (-1.0f + sp) + 1e-5f;
   const float norm_w2 = nw2 + 1e-9f;
   const float coef = m_wtu - wtu;
   const float th = f_tanh<FAST>(wz + b);
   const float dth = 1.0f - th * th;
-  float sd = 0.0f;
 #pragma unroll
   for (int i = 0; i < DPL; ++i) {
     const float uh = u[i] + coef * f_div_acc<FAST>(w[i], norm_w2);  // 0 on inactive dims
     z[i] = z[i] + uh * th;
-    sd += uh * (dth * w[i]);
   }
-  return f_log<FAST>(fabsf(1.0f + gsum<G>(sd)));
+  const float qd = fmaf(-coef * 1e-9f, f_div<FAST>(1.0f, norm_w2), sp + 1e-5f);
+  return f_log<FAST>(fabsf(fmaf(th, th, dth * qd)));
 }
 
 template <int G, int DPL, bool FAST, bool FULL = false, bool LDJ = true>

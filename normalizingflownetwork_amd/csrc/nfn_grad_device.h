@@ -49,7 +49,8 @@ __device__ __forceinline__ void planar_bwd(const float (&z)[DM], float (&a)[DM],
   }
   s += p[2 * d];
   nw2 += 1e-9f;
-  const float m = (-1.0f + softplus_tf<FAST>(wtu)) + 1e-5f;  // = w . u_hat (the constraint)
+  const float sp = softplus_alpha<FAST>(wtu);  // relative accuracy as w.u -> -inf
+  const float m = (-1.0f + sp) + 1e-5f;        // = w . u_hat (the constraint)
   const float c = m - wtu;
   const float sg = f_sigmoid<FAST>(wtu);
   const float cn = f_div_acc<FAST>(c, nw2);
@@ -67,12 +68,14 @@ __device__ __forceinline__ void planar_bwd(const float (&z)[DM], float (&a)[DM],
   float ua = 0.0f;
 #pragma unroll
   for (int j = 0; j < DM; ++j) {
-    uh[j] = fmaf(cn, w[j], u[j]);
+    // d = 1: (1e-9 u + m w) / n, the well-conditioned form of planar_step
+    uh[j] = d == 1 ? f_div_acc<FAST>(fmaf(u[j], 1e-9f, m * w[j]), nw2) : fmaf(cn, w[j], u[j]);
     ua += uh[j] * a[j];
   }
-  // w . u_hat = wtu + c |w|^2 / n = m - c * 1e-9 / n, without the d-term cancellation
+  // w . u_hat = wtu + c |w|^2 / n = m - c * 1e-9 / n, without the d-term cancellation;
+  // det = 1 + hp q = h^2 + hp (softplus + 1e-5 - c 1e-9 / n), without the q -> -1 one
   const float q = m - cn * 1e-9f;
-  const float hpd = gl * f_div<FAST>(hp, 1.0f + hp * q);
+  const float hpd = gl * f_div<FAST>(hp, fmaf(h, h, hp * ((sp + 1e-5f) - cn * 1e-9f)));
   const float Ss = hp * ua - 2.0f * q * h * hpd;
   float G[DM];
   float wG = 0.0f;
@@ -195,11 +198,13 @@ __device__ __forceinline__ void sp_sig1(float x, float& sp, float& sg) {
 }
 
 // z-only forward steps (the backward needs each flow's input, not its log-det).
+// (planar1_fast's z update, bitwise)
 __device__ __forceinline__ void planar1_z(float& z, float u, float wraw, float b) {
   const float w = wraw + 1.0f;
   const float wtu = w * u;
-  const float coef = sp_fast1(wtu) - (wtu + (1.0f - 1e-5f));
-  const float uh = fmaf(coef, f_div_acc<true>(w, fmaf(w, w, 1e-9f)), u);
+  const float nw2 = fmaf(w, w, 1e-9f);
+  const float m = softplus_alpha<true>(wtu) - (1.0f - 1e-5f);
+  const float uh = planar1_uh(u, w, nw2, __builtin_amdgcn_rcpf(nw2), m);
   const float E = __builtin_amdgcn_exp2f(fmaf(w, z, b) * (2.0f * kLog2e));
   z = fmaf(uh, 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f)), z);
 }
@@ -220,21 +225,22 @@ __device__ __forceinline__ void planar1_bwd(float z, float& a, float p0, float p
   const float w = p1 + 1.0f;
   const float wtu = w * u;
   float sp, sg;
-  sp_sig1(wtu, sp, sg);
+  sp_sig1<true>(wtu, sp, sg);
   const float m = (sp - 1.0f) + 1e-5f;
   const float c = m - wtu;
   const float nw2 = fmaf(w, w, 1e-9f);
   const float rn = __builtin_amdgcn_rcpf(nw2);
   const float q0 = c * rn;
   const float cn = fmaf(fmaf(-nw2, q0, c), rn, q0);  // c / n, Newton-refined
-  const float uh = fmaf(cn, w, u);
+  const float uh = planar1_uh(u, w, nw2, rn, m);     // (planar1_fast's well-conditioned form)
   const float s = fmaf(w, z, p2);
   const float E = __builtin_amdgcn_exp2f(fabsf(s) * (-2.0f * kLog2e));
   const float rE = __builtin_amdgcn_rcpf(1.0f + E);
   const float h = copysignf((1.0f - E) * rE, s);
   const float hp = 4.0f * E * rE * rE;
   const float q = fmaf(-cn, 1e-9f, m);
-  const float hpd = gl * hp * __builtin_amdgcn_rcpf(fmaf(hp, q, 1.0f));
+  // det = 1 + hp q = h^2 + hp (softplus + 1e-5 - cn 1e-9): no cancellation as q -> -1
+  const float hpd = gl * hp * __builtin_amdgcn_rcpf(fmaf(h, h, hp * fmaf(-cn, 1e-9f, sp + 1e-5f)));
   const float Ss = fmaf(hp, uh * a, -2.0f * q * h * hpd);
   const float G = fmaf(h, a, hpd * w);
   const float wGn = w * G * rn;
@@ -579,7 +585,7 @@ __device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[
   const float s = gsum<G>(swz) + p[2 * d];
   float sp, sg;
   if constexpr (FAST) {
-    sp_sig1(wtu, sp, sg);
+    sp_sig1<true>(wtu, sp, sg);  // softplus relative-accurate as w.u -> -inf
   } else {
     sp = softplus_tf<false>(wtu);
     sg = f_sigmoid<false>(wtu);
@@ -604,7 +610,8 @@ __device__ __forceinline__ void planar_gd_bwd(const float (&z)[DPL], float (&a)[
   }
   const float ua = gsum<G>(sua);
   const float q = m - cn * 1e-9f;
-  const float hpd = gl * f_div<FAST>(hp, 1.0f + hp * q);
+  // det = 1 + hp q = h^2 + hp (softplus + 1e-5 - cn 1e-9) (planar_bwd)
+  const float hpd = gl * f_div<FAST>(hp, fmaf(h, h, hp * ((sp + 1e-5f) - cn * 1e-9f)));
   const float Ss = hp * ua - 2.0f * q * h * hpd;
   float Gv[DPL];
   float swG = 0.0f;

@@ -8,6 +8,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <vector>
 
 #include "nfn_device.h"
 
@@ -33,20 +36,52 @@ inline int64_t cap_grid(int64_t grid, const ChainArgs& a) {
   return a.grid_cap > 0 ? std::min(grid, a.grid_cap) : grid;
 }
 
+// CU count of the current device, queried once per device and process (a launch
+// below 2^20 samples takes ~10 us, so no runtime query sits on the launch path).
 inline int cu_count() {
-  int dev = 0, n = 0;
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cached[kMaxDev] = {};
+  int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev >= 0 && dev < kMaxDev) {
+    const int c = cached[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
+  int n = 0;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  if (dev >= 0 && dev < kMaxDev) cached[dev].store(n, std::memory_order_relaxed);
   return n;
+}
+
+// Resident workgroups per CU of (kernel, threads, LDS bytes): the occupancy query runs
+// once per key and process.  (The answer depends on the kernel's resources only, which
+// are the same on every MI355X of a node.)
+inline int occupancy_cached(const void* kfn, int threads, size_t lds) {
+  struct Key {
+    const void* f;
+    int threads;
+    size_t lds;
+    int occ;
+  };
+  static std::mutex mu;
+  static std::vector<Key> table;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const Key& k : table)
+      if (k.f == kfn && k.threads == threads && k.lds == lds) return k.occ;
+  }
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, threads, lds) != hipSuccess || occ <= 0) return 1;
+  std::lock_guard<std::mutex> g(mu);
+  if (table.size() < 4096) table.push_back({kfn, threads, lds, occ});
+  return occ;
 }
 
 // Persistent grid: CUs x resident workgroups (occupancy query, or NFN_WG_PER_CU).
 template <typename K>
 inline int64_t persistent_grid(K kfn, int threads, size_t lds, int64_t units) {
   int occ = env_int("NFN_WG_PER_CU", 0);
-  if (occ <= 0) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, threads, lds) != hipSuccess || occ <= 0) occ = 1;
-  }
+  if (occ <= 0) occ = occupancy_cached(reinterpret_cast<const void*>(kfn), threads, lds);
   return std::min<int64_t>(units, (int64_t)cu_count() * occ);
 }
 

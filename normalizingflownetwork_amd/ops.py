@@ -7,6 +7,7 @@ There is no CPU fallback — without a GPU these raise ``RuntimeError``.
 
 from __future__ import annotations
 
+import collections
 import ctypes
 import threading
 from typing import Optional, Sequence
@@ -68,21 +69,29 @@ def total_param_size(flow_types: Sequence[str], n_dims: int, trainable_base: boo
     return sum(param_size(f, n_dims) for f in flow_types) + (2 * n_dims if trainable_base else 0)
 
 
-_workspaces: dict = {}
+_workspaces: "collections.OrderedDict" = collections.OrderedDict()
 _ws_lock = threading.Lock()
+# (device, stream) workspaces kept at once; the least recently used is dropped beyond
+# this (pooled / side streams come and go: fit's capture stream, the bench's ring).
+WORKSPACE_CACHE_ENTRIES = 8
 
 
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
-    """The zero-initialised workspace of the current (device, stream): calls are ordered on
-    their stream, so calls in flight on different streams never share partials, the
-    posterior's split region or the finishing ticket (which every call leaves at 0, so a
-    workspace is zeroed once, when it is created or grown)."""
+    """The workspace of the current (device, stream): calls are ordered on their stream,
+    so calls in flight on different streams never share partials, the posterior's split
+    region or the finishing ticket.  No initialisation is needed (ABI 200: every summed
+    call clears its ticket on the stream).  Dropping an entry is safe: its memory returns
+    to the caching allocator's pool of the SAME stream, so a later allocation that reuses
+    it is ordered after the calls that used it."""
     key = (device.index, int(torch.cuda.current_stream(device).cuda_stream))
     with _ws_lock:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < n_doubles:
-            ws = torch.zeros(max(2, n_doubles), dtype=torch.float64, device=device)
-            _workspaces[key] = ws
+            ws = torch.empty(max(2, n_doubles), dtype=torch.float64, device=device)
+        _workspaces[key] = ws
+        _workspaces.move_to_end(key)
+        while len(_workspaces) > WORKSPACE_CACHE_ENTRIES:
+            _workspaces.popitem(last=False)
         return ws
 
 

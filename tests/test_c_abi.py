@@ -44,7 +44,12 @@ def test_exported_symbols_are_c_linkage(native_lib):
 
 
 def test_version(native_lib):
-    assert native_lib.nfn_version() == 100
+    # 200: out_sum is double[2] and the workspace needs no initialisation (include/nfn.h)
+    from normalizingflownetwork_amd import _lib
+
+    assert native_lib.nfn_version() == _lib.ABI_VERSION == 200
+    hdr = open(os.path.join(REPO, "include", "nfn.h")).read()
+    assert re.search(r"#define NFN_ABI_VERSION 200\b", hdr)
 
 
 def _ids(*names):
@@ -84,6 +89,13 @@ def test_bad_arguments_are_rejected_before_launch(native_lib):
     assert lib.nfn_chain_logprob_f32(fake, 1, fake, 8, 10, 1, ids, 2, 1, None, None, fake, fake, None, None) == -3
     # NULL y
     assert lib.nfn_chain_logprob_f32(None, 1, fake, 8, 10, 1, ids, 2, 1, None, None, fake, None, None, None) == -3
+    # a batch longer than one chunk (2^24 + 1 samples runs as two launches) is validated as a
+    # whole before the first launch: no chunk may run before the call is rejected
+    big = (1 << 24) + 1
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 8, big, 1, ids, 2, 1, None, None, fake, fake, None, None) == -3
+    assert b"workspace" in lib.nfn_last_error()
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 8, big, 1, ids, 2, 1, fake, None, fake, None, None, None) == -3
+    assert lib.nfn_chain_logprob_f32(fake, 1, fake, 4, big, 1, ids, 2, 1, None, None, fake, None, None, None) == -1
     # bad flow id in the single-flow entry point
     assert lib.nfn_flow_fwd_ldj_f32(9, fake, 1, fake, 3, 10, 1, fake, fake, None) == -2
     assert lib.nfn_flow_fwd_ldj_f32(0, fake, 1, fake, 2, 10, 1, fake, fake, None) == -1  # stride < 2d+1

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from oracle import nfn_oracle as O
+from parity import check_bound, check_forward, check_grad
 
 pytestmark = pytest.mark.gpu
 
@@ -45,9 +46,8 @@ def test_dense_matches_oracle(math_mode, ft, d, H, B):
     ref64 = O.chain_log_prob(y, t64, ft, d, True, np.float64)
     ref32 = O.chain_log_prob(y, t32, ft, d, True, np.float32)
     got = out.cpu().numpy()
+    check_forward(got, ref64, ref32, f"dense {ft[:2]}x{len(ft)} d={d} H={H} B={B} [{math_mode}]", kind="dense")
     bound = O.tolerance_bound(ref64, ref32)
-    bad = ~(np.abs(got - ref64) <= bound)
-    assert not bad.any(), (int(bad.sum()), got[bad][:4], ref64[bad][:4])
     assert abs(s.item() - ref64.sum()) <= bound.sum() + 1e-6 * abs(ref64.sum())
 
 
@@ -66,7 +66,7 @@ def test_dense_with_normalisation_and_fallback(gpu):
                                           torch.from_numpy(W).cuda(), bb, ft, d, True, ym, ys)
         ref64 = O.log_pdf(y, t64, ft, d, True, ym, ys, np.float64)
         ref32 = O.log_pdf(y, t32, ft, d, True, ym, ys, np.float32)
-        assert np.all(np.abs(out.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32)), H
+        check_forward(out.cpu().numpy(), ref64, ref32, f"dense normalised H={H} bias={bias}", kind="dense")
 
 
 def _post_case(ft, d, H, B, S, seed, shared_h=False, bias=True):
@@ -105,9 +105,9 @@ def test_posterior_dense_matches_oracle(math_mode, ft, d, H, B, S, shared):
     ref32 = O.posterior_lse(y, t32, ft, d, True, dtype=np.float32)
     got = out.cpu().numpy()
     ok = np.isfinite(ref64)
+    check_forward(got, ref64, ref32, f"posterior dense {ft[:2]}x{len(ft)} d={d} H={H} S={S} shared={shared} "
+                  f"[{math_mode}]", nonfinite="match", kind="dense")
     bound = O.tolerance_bound(ref64, ref32)
-    bad = ok & ~(np.abs(got - ref64) <= bound)
-    assert not bad.any(), (int(bad.sum()), got[bad][:4], ref64[bad][:4])
     assert abs(s.item() - ref64[ok].sum()) <= bound[ok].sum() + 1e-6 * abs(ref64[ok].sum()) or not ok.all()
 
 
@@ -125,7 +125,7 @@ def test_posterior_dense_normalised_nobias_and_fallback(gpu):
                                          torch.from_numpy(W).cuda(), bb, ft, d, True, ym, ys)
         ref64 = O.posterior_lse(y, t64, ft, d, True, ym, ys, np.float64)
         ref32 = O.posterior_lse(y, t32, ft, d, True, ym, ys, np.float32)
-        assert np.all(np.abs(out.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32)), H
+        check_forward(out.cpu().numpy(), ref64, ref32, f"posterior dense normalised H={H} bias={bias}", kind="dense")
 
 
 def test_posterior_dense_full_size_c5_sampled(gpu):
@@ -151,7 +151,7 @@ def test_posterior_dense_full_size_c5_sampled(gpu):
     ref64 = O.posterior_lse(ys, t64, ft, d, True, dtype=np.float64)
     ref32 = O.posterior_lse(ys, t32, ft, d, True, dtype=np.float32)
     got = out[idx.cuda()].cpu().numpy()
-    assert np.all(np.abs(got - ref64) <= O.tolerance_bound(ref64, ref32))
+    check_forward(got, ref64, ref32, "posterior dense C5 sample", kind="dense")
     assert abs(s.item() - out.double().sum().item()) <= 1e-9 * abs(s.item()) + 1e-6
 
 
@@ -183,13 +183,13 @@ def test_dense_grad_matches_oracle(math_mode, ft, d, H, B):
     bW = np.abs(h64).T @ bt + 1e-5 * (np.abs(h64).T @ np.abs(gt64)) + 1e-6
     bb = bt.sum(0) + 1e-5 * np.abs(gt64).sum(0) + 1e-6
     for got, ref, bound, what in ((gh, gh_ref, bh, "dh"), (gW, gW_ref, bW, "dW"), (gb, gb_ref, bb, "db")):
-        err = np.abs(got.cpu().numpy().astype(np.float64) - ref)
-        assert (err <= bound).all(), f"{what}: max err/bound {np.max(err / bound):.3g}"
-    ey = np.abs(gy.cpu().numpy() - gy64)
-    assert (ey <= G.grad_tolerance(gy64, dev_y)).all(), "dy"
+        check_bound(got.cpu().numpy(), ref, bound, f"dense grad {what} {ft[:2]}x{len(ft)} d={d} H={H} [{math_mode}]",
+                    kind="dense_grad")
+    check_grad(gy.cpu().numpy(), gy64, dev_y, f"dense grad dy {ft[:2]}x{len(ft)} d={d} H={H} [{math_mode}]")
     ref64 = O.chain_log_prob(y, t64, ft, d, True, np.float64)
     ref32 = O.chain_log_prob(y, t32, ft, d, True, np.float32)
-    assert np.all(np.abs(lp.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32))
+    check_forward(lp.cpu().numpy(), ref64, ref32, f"dense grad log_prob {ft[:2]}x{len(ft)} d={d} H={H} [{math_mode}]",
+                  kind="dense_grad")
     # deterministic: a second run is bitwise identical
     _, gh2, gW2, gb2, _ = ops.chain_log_prob_dense_grad(torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(),
                                                          torch.from_numpy(W).cuda(), torch.from_numpy(b).cuda(), ft,
@@ -270,11 +270,11 @@ def test_dense1_grad_kernel_shapes(gpu, ft, H, B, trainable, g_none):
     bW = np.abs(h64).T @ bt + 1e-5 * (np.abs(h64).T @ np.abs(gt64)) + 1e-6
     bb = bt.sum(0) + 1e-5 * np.abs(gt64).sum(0) + 1e-6
     for got, ref, bound, what in ((gh, gh_ref, bh, "dh"), (gW, gW_ref, bW, "dW"), (gb, gb_ref, bb, "db")):
-        err = np.abs(got.cpu().numpy().astype(np.float64) - ref)
-        assert (err <= bound).all(), f"{what}: max err/bound {np.max(err / bound):.3g}"
-    ey = np.abs(gy.cpu().numpy() - gy64 / 2.0)
-    assert (ey <= G.grad_tolerance(gy64 / 2.0, dev_y / 2.0)).all(), "dy"
+        check_bound(got.cpu().numpy(), ref, bound, f"dense1 grad {what} {ft[:2]}x{len(ft)} H={H} B={B}",
+                    kind="dense_grad")
+    check_grad(gy.cpu().numpy(), gy64 / 2.0, dev_y / 2.0, f"dense1 grad dy {ft[:2]}x{len(ft)} H={H} B={B}")
     t64 = h64 @ W64 + b.astype(np.float64)
     ref64 = O.chain_log_prob(z, t64, ft, d, trainable, np.float64) - np.log(2.0)
     ref32 = O.chain_log_prob(z, t32, ft, d, trainable, np.float32) - np.float32(np.log(2.0))
-    assert np.all(np.abs(lp.cpu().numpy() - ref64) <= O.tolerance_bound(ref64, ref32))
+    check_forward(lp.cpu().numpy(), ref64, ref32, f"dense1 grad log_prob {ft[:2]}x{len(ft)} H={H} B={B}",
+                  kind="dense_grad")

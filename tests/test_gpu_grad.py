@@ -13,6 +13,7 @@ import pytest
 import torch
 
 from conftest import CHAIN_FIXTURES, load_golden
+from parity import check_forward, check_grad
 from oracle import nfn_grad_oracle as G
 
 pytestmark = pytest.mark.gpu
@@ -25,21 +26,7 @@ def _grads_ref(y, t, ft, d, tr, ym=None, ys=None, g=None):
     return gt64, dev_t, gy64, dev_y
 
 
-def _check(got, ref64, dev32, what, row_scale=True):
-    got = np.asarray(got, np.float64)
-    assert got.shape == ref64.shape, (what, got.shape, ref64.shape)
-    if got.size == 0:
-        return
-    bound = G.grad_tolerance(ref64, dev32, row_scale=row_scale)
-    err = np.abs(got - ref64)
-    finite = np.isfinite(ref64)
-    assert np.array_equal(np.isfinite(got), finite), f"{what}: non-finite pattern differs"
-    bad = finite & ~(err <= bound)
-    if bad.any():
-        i = np.argwhere(bad)[0]
-        raise AssertionError(f"{what}: {bad.sum()} elements out of tolerance; first {tuple(i)}: "
-                             f"got {got[tuple(i)]!r} ref64 {ref64[tuple(i)]!r} bound {bound[tuple(i)]!r}; "
-                             f"max err/bound {np.max(err[finite] / bound[finite]):.3g}")
+_check = check_grad
 
 
 def _run(gpu, y, t, ft, d, tr, ym=None, ys=None, g=None):
@@ -73,10 +60,7 @@ def test_grad_fixture_vs_oracle(gpu, math_mode, name):
     # the backward's own log_prob equals the forward oracle
     from oracle import nfn_oracle as O
 
-    ref = fx["ref64"][:B]
-    bound = O.tolerance_bound(ref, fx["ref32"][:B])
-    ok = np.isfinite(ref)
-    assert np.all(np.abs(lp[ok] - ref[ok]) <= bound[ok]), name
+    check_forward(lp, fx["ref64"][:B], fx["ref32"][:B], f"{name} backward's log_prob [{math_mode}]", nonfinite="match")
 
 
 @pytest.mark.parametrize("ft,d", [(("planar", "radial") * 5, 1), (("affine", "planar", "radial"), 3),

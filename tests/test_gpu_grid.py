@@ -8,6 +8,7 @@ import pytest
 import torch
 
 from oracle import nfn_oracle as O
+from parity import check_forward
 
 pytestmark = pytest.mark.gpu
 
@@ -40,12 +41,11 @@ def test_grid_matches_oracle(math_mode, ft, d, B, G):
     out = ops.chain_log_prob_grid(torch.from_numpy(yg).cuda(), torch.from_numpy(t).cuda(), ft, d, True)
     r64, r32 = _ref(yg, t, ft, d, True)
     assert out.shape == (G, B)
-    bound = O.tolerance_bound(r64, r32)
-    assert np.all(np.abs(out.cpu().numpy() - r64) <= bound)
+    check_forward(out.cpu().numpy(), r64, r32, f"grid {ft[:2]}x{len(ft)} d={d} B={B} G={G} [{math_mode}]", kind="grid")
     ym, ys = np.linspace(-0.2, 0.3, d).astype(np.float32), np.linspace(0.5, 2.0, d).astype(np.float32)
     outn = ops.chain_log_prob_grid(torch.from_numpy(yg).cuda(), torch.from_numpy(t).cuda(), ft, d, True, ym, ys)
     r64, r32 = _ref(yg, t, ft, d, True, ym, ys)
-    assert np.all(np.abs(outn.cpu().numpy() - r64) <= O.tolerance_bound(r64, r32))
+    check_forward(outn.cpu().numpy(), r64, r32, f"grid normalised {ft[:2]}x{len(ft)} d={d} [{math_mode}]", kind="grid")
     # a broadcast parameter row gives the same column for every b
     out1 = ops.chain_log_prob_grid(torch.from_numpy(yg).cuda(), torch.from_numpy(t[:1]).cuda(), ft, d, True)
     assert torch.equal(out1[:, 0], out[:, 0])

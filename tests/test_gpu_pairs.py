@@ -14,6 +14,7 @@ import torch
 
 from oracle import nfn_grad_oracle as G
 from oracle import nfn_oracle as O
+from parity import check_forward, check_grad
 
 pytestmark = pytest.mark.gpu
 
@@ -45,9 +46,7 @@ def test_pair_form_forward_and_posterior(ft, gpu):
     with np.errstate(all="ignore"):
         r64 = O.chain_log_prob(y, t, ft, 1, True, np.float64)
         r32 = O.chain_log_prob(y, t, ft, 1, True, np.float32)
-    got = lp.cpu().numpy()
-    ok = np.isfinite(r64)
-    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    check_forward(lp.cpu().numpy(), r64, r32, f"pairs {_ids(ft)} forward", nonfinite="match")
     # posterior: S draws of t per sample
     S, Bp = 3, 333
     tp = (0.7 * rng.standard_normal((S, Bp, P))).astype(np.float32)
@@ -55,9 +54,7 @@ def test_pair_form_forward_and_posterior(ft, gpu):
     with np.errstate(all="ignore"):
         p64 = O.posterior_lse(y[:Bp], tp, ft, 1, True)
         p32 = O.posterior_lse(y[:Bp], tp, ft, 1, True, dtype=np.float32)
-    got = out.cpu().numpy()
-    ok = np.isfinite(p64)
-    assert (np.abs(got[ok] - p64[ok]) <= O.tolerance_bound(p64[ok], p32[ok])).all()
+    check_forward(out.cpu().numpy(), p64, p32, f"pairs {_ids(ft)} posterior", nonfinite="match")
 
 
 @pytest.mark.parametrize("ft", [p for p in PROGRAMS if len(p) <= 6], ids=_ids)
@@ -74,16 +71,11 @@ def test_pair_form_backward(ft, gpu):
     lp, gt, gy = ops.chain_log_prob_grad(torch.from_numpy(y).to(gpu), torch.from_numpy(t).to(gpu), ft, 1, True,
                                          g_out=torch.from_numpy(g).to(gpu), want_logp=True)
     for got, ref, dev, what in ((gt, gt64, dev_t, "d/dt"), (gy, gy64, dev_y, "d/dy")):
-        got = got.cpu().numpy().astype(np.float64).reshape(ref.shape)
-        fin = np.isfinite(ref)
-        assert np.array_equal(np.isfinite(got), fin), what
-        assert (np.abs(got[fin] - ref[fin]) <= G.grad_tolerance(ref, dev)[fin]).all(), what
+        check_grad(got.cpu().numpy().reshape(ref.shape), ref, dev, f"pairs {_ids(ft)} {what}")
     with np.errstate(all="ignore"):
         r64 = O.chain_log_prob(y, t, ft, 1, True, np.float64)
         r32 = O.chain_log_prob(y, t, ft, 1, True, np.float32)
-    got = lp.cpu().numpy()
-    ok = np.isfinite(r64)
-    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    check_forward(lp.cpu().numpy(), r64, r32, f"pairs {_ids(ft)} backward's log_prob", nonfinite="match")
 
 
 @pytest.mark.parametrize("ft", [("planar", "radial") * 5, ("affine",) * 15, ("planar", "radial", "planar", "affine", "radial")],

@@ -19,6 +19,7 @@ import torch
 
 from conftest import load_golden
 from oracle import nfn_oracle as O
+from parity import check_forward
 
 pytestmark = pytest.mark.gpu
 C2 = ("planar", "radial") * 5
@@ -71,7 +72,7 @@ def test_posterior_split_stays_in_workspace(S, B, gpu):
     idx = np.r_[0:64, rng.integers(0, B, 192), B - 64:B]
     r64 = O.posterior_lse(y[idx], t[:, idx], C2, 1, True)
     r32 = O.posterior_lse(y[idx], t[:, idx], C2, 1, True, dtype=np.float32)
-    assert (np.abs(got[idx] - r64) <= O.tolerance_bound(r64, r32)).all()
+    check_forward(got[idx], r64, r32, f"posterior split S={S} B={B}")
 
 
 @pytest.mark.parametrize("d,ft", [(20, ("radial", "radial", "affine")), (24, ("radial", "radial", "affine")),
@@ -105,7 +106,7 @@ def test_group_partials_stay_in_workspace(d, ft, B, gpu):
         r64 = O.chain_log_prob(y, t, ft, d, True, np.float64)
         r32 = O.chain_log_prob(y, t, ft, d, True, np.float32)
     fin = np.isfinite(r64)  # an affine scale 1 + t of 0 is a legitimate -inf log-density
-    assert (np.abs(got[fin] - r64[fin]) <= O.tolerance_bound(r64[fin], r32[fin])).all()
+    check_forward(got, r64, r32, f"group partials d={d} B={B}", nonfinite="match")
     assert (~np.isfinite(got[~fin])).all()
     assert osum[1].item() == float((~np.isfinite(got)).sum())  # the non-finite count
     assert int(ws[1].item()) == 0  # the finishing ticket is left at zero
@@ -219,9 +220,7 @@ def test_c4_global_batch_on_one_device(gpu):
     yn, tn = y[idx].cpu().numpy(), t[idx].cpu().numpy()
     r64 = O.chain_log_prob(yn, tn, C2, 1, True, np.float64)
     r32 = O.chain_log_prob(yn, tn, C2, 1, True, np.float32)
-    got = lp[idx].cpu().numpy().astype(np.float64)
-    ok = np.isfinite(r64)
-    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    check_forward(lp[idx].cpu().numpy(), r64, r32, "C4 global batch on one device, sample", nonfinite="match")
     del t
     torch.cuda.empty_cache()
 
@@ -282,8 +281,61 @@ def test_chunked_batch(ft, d, B, gpu):
     yn, tn = y[idx].cpu().numpy(), t[idx].cpu().numpy()
     r64 = O.chain_log_prob(yn, tn, ft, d, True, np.float64)
     r32 = O.chain_log_prob(yn, tn, ft, d, True, np.float32)
-    got = out[idx].cpu().numpy().astype(np.float64)
-    ok = np.isfinite(r64)
-    assert (np.abs(got[ok] - r64[ok]) <= O.tolerance_bound(r64[ok], r32[ok])).all()
+    check_forward(out[idx].cpu().numpy(), r64, r32, f"chunked d={d} B={B} sample", nonfinite="match")
     del t
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("kind", ["chain", "chain_chunked", "posterior", "dense"])
+def test_uninitialised_workspace(kind, gpu):
+    """ABI 200: a workspace from plain allocation — here filled with garbage,
+    the finishing ticket included — gives the same fp64 sum as a zeroed one: every summed
+    call clears its ticket on the stream before launching."""
+    from normalizingflownetwork_amd import _lib
+
+    lib = _lib.load()
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    B = {"chain": 100_000, "chain_chunked": (1 << 24) + 77, "posterior": 30_000, "dense": 50_000}[kind]
+    y = torch.randn((B, 1), generator=gen, device="cuda")
+    ids, k = _ids(C2)
+    p_ids = ctypes.cast(ids, ctypes.c_void_p)
+    res = []
+    for garbage in (False, True):
+        t = None
+        if kind == "posterior":
+            n = int(lib.nfn_posterior_workspace_doubles(B, 1, 32))
+        else:
+            n = int(lib.nfn_chain_workspace_doubles(B, 1, 32))
+        ws = torch.zeros((n,), dtype=torch.float64, device="cuda")
+        if garbage:
+            ws.view(torch.int32).fill_(0x5A5A5A5A)  # a non-zero ticket (workspace[1]), garbage pairs
+        osum = torch.full((2,), -1.0, dtype=torch.float64, device="cuda")
+        out = torch.empty((B,), dtype=torch.float32, device="cuda")
+        if kind in ("chain", "chain_chunked"):
+            t = torch.randn((B, 32), generator=torch.Generator(device="cuda").manual_seed(1), device="cuda")
+            rc = lib.nfn_chain_logprob_f32(y.data_ptr(), 1, t.data_ptr(), 32, B, 1, p_ids, k, 1, None, None,
+                                           out.data_ptr(), osum.data_ptr(), ws.data_ptr(), None)
+        elif kind == "posterior":
+            S = 4
+            t = torch.randn((S, B, 32), generator=torch.Generator(device="cuda").manual_seed(1), device="cuda")
+            rc = lib.nfn_posterior_lse_f32(y.data_ptr(), 1, t.data_ptr(), B * 32, 32, S, B, 1, p_ids, k, 1, None,
+                                           None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(), None)
+        else:
+            H = 16
+            g1 = torch.Generator(device="cuda").manual_seed(1)
+            h = torch.randn((B, H), generator=g1, device="cuda")
+            W = 0.3 * torch.randn((H, 32), generator=g1, device="cuda")
+            rc = lib.nfn_chain_logprob_dense_f32(y.data_ptr(), 1, h.data_ptr(), H, H, W.data_ptr(), None, B, 1, p_ids,
+                                                 k, 1, None, None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(),
+                                                 None)
+        _lib.check(rc, kind)
+        torch.cuda.synchronize()
+        assert int(ws[1].item()) == 0, "the ticket is left at zero"
+        res.append((osum.clone(), out.clone()))
+        del t
+    assert torch.equal(res[0][1], res[1][1])
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
+    fin = torch.isfinite(res[0][1])
+    if fin.all():
+        assert float(res[0][0][0].item()) == pytest.approx(float(res[0][1].double().sum().item()), rel=1e-12)
     torch.cuda.empty_cache()
