@@ -137,7 +137,7 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *                workgroup (fixed summation order: bitwise deterministic; no extra launch)
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
  *                Needs no initialisation (e.g. a plain hipMalloc): a summed call clears
- *                the ticket with a 4-byte stream-ordered memset before its launch.
+ *                the ticket (workspace[1]) with a stream-ordered memset before its launch.
  *                Layout: workspace[0] = number n of per-workgroup pairs written,
  *                workspace[1] = the finishing ticket, workspace[2 + 2i] /
  *                workspace[3 + 2i] = workgroup i's fp64 partial sum / non-finite count.

@@ -182,10 +182,10 @@ int32_t check_hip(const char* what) {
 }
 
 // The in-kernel finish counts workgroups on a ticket at workspace[1]; it is cleared on the
-// stream before every summed launch (a 4-byte memset node, graph-capturable), so the
+// stream before every summed launch (an 8-byte memset node, graph-capturable), so the
 // workspace needs no initialisation and a call aborted mid-way cannot poison the next.
 int32_t reset_ticket(double* workspace, hipStream_t s) {
-  if (hipMemsetAsync(workspace + 1, 0, sizeof(uint32_t), s) != hipSuccess) return check_hip("hipMemsetAsync (ticket)");
+  if (hipMemsetAsync(workspace + 1, 0, sizeof(double), s) != hipSuccess) return check_hip("hipMemsetAsync (ticket)");
   return NFN_OK;
 }
 

@@ -253,12 +253,27 @@ __device__ __forceinline__ float softplus_alpha(float x) {
   }
 }
 
+// tanh with RELATIVE accuracy (a few ulp) everywhere.  1 - 2 / (1 + e^{2a}) has an
+// absolute error of ~1e-7, i.e. a large relative one as a -> 0; a planar step multiplies
+// tanh by u_hat, which reaches ~1 / |w| when w -> 0 (u_hat ~ m / w), so the absolute
+// error became a z error of ~1e-7 / |w| (C2 full batch: log_prob off by up to 2e-4 on
+// 2e-5 of the samples, tests/test_gpu_fullbatch.py).  Below |a| = 0.3 the Taylor
+// polynomial to a^9 (truncation < 5e-8 relative); above it the exp form (< 4e-7).
+__device__ __forceinline__ float tanh_fast(float a) {
+  const float E = __builtin_amdgcn_exp2f(a * (2.0f * kLog2e));
+  const float te = 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));  // saturates to +-1 cleanly
+  const float a2 = a * a;
+  float p = fmaf(a2, 62.0f / 2835.0f, -17.0f / 315.0f);
+  p = fmaf(a2, p, 2.0f / 15.0f);
+  p = fmaf(a2, p, -1.0f / 3.0f);
+  const float tp = fmaf(a * a2, p, a);
+  return fabsf(a) < 0.3f ? tp : te;
+}
+
 template <bool FAST>
 __device__ __forceinline__ float f_tanh(float a) {
   if constexpr (FAST) {
-    // 1 - 2 / (1 + e^{2a}): absolute error ~1e-7, saturates to +-1 cleanly.
-    const float E = __builtin_amdgcn_exp2f(a * (2.0f * kLog2e));
-    return 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));
+    return tanh_fast(a);
   } else {
     return tanhf(a);
   }
@@ -456,11 +471,11 @@ __device__ __forceinline__ float sp_fast1(float x) { return softplus_tf<true>(x)
 //   m = -1 + softplus(wu) + 1e-5 (softplus relative-accurate as wu -> -inf),
 //   u_hat = u + (m - wu) w / (w^2 + 1e-9) = (1e-9 u + m w) / (w^2 + 1e-9),
 //   det = 1 + (1 - th^2) w u_hat = th^2 + (1 - th^2)(softplus(wu) + 1e-5 - (m - wu) 1e-9 / (w^2 + 1e-9)),
-//   tanh(x) = 1 - 2 / (1 + e^{2x})
-__device__ __forceinline__ float planar1_uh(float u, float w, float nw2, float rn, float m) {
-  const float num = fmaf(u, 1e-9f, m * w);
-  const float q0 = num * rn;
-  return fmaf(fmaf(-nw2, q0, num), rn, q0);  // num / nw2, Newton-refined
+//   th = tanh_fast(w z + b) (relative accuracy: u_hat th with u_hat ~ m / w)
+// (no cancellation follows the quotient, so v_rcp_f32's 1-ulp error is not amplified:
+// no Newton step)
+__device__ __forceinline__ float planar1_uh(float u, float w, float rn, float m) {
+  return fmaf(u, 1e-9f, m * w) * rn;
 }
 
 __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, float b) {
@@ -470,10 +485,9 @@ __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, flo
   const float rn = __builtin_amdgcn_rcpf(nw2);
   const float sp = softplus_alpha<true>(wtu);
   const float m = sp - (1.0f - 1e-5f);
-  const float uh = planar1_uh(u, w, nw2, rn, m);
+  const float uh = planar1_uh(u, w, rn, m);
   const float qd = fmaf((wtu - m) * 1e-9f, rn, sp + 1e-5f);
-  const float E = __builtin_amdgcn_exp2f(fmaf(w, z, b) * (2.0f * kLog2e));
-  const float th = 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));
+  const float th = tanh_fast(fmaf(w, z, b));
   z = fmaf(uh, th, z);
   return fmaf(th, th, fmaf(-th, th, 1.0f) * qd);
 }

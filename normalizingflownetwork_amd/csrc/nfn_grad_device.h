@@ -204,9 +204,8 @@ __device__ __forceinline__ void planar1_z(float& z, float u, float wraw, float b
   const float wtu = w * u;
   const float nw2 = fmaf(w, w, 1e-9f);
   const float m = softplus_alpha<true>(wtu) - (1.0f - 1e-5f);
-  const float uh = planar1_uh(u, w, nw2, __builtin_amdgcn_rcpf(nw2), m);
-  const float E = __builtin_amdgcn_exp2f(fmaf(w, z, b) * (2.0f * kLog2e));
-  z = fmaf(uh, 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f)), z);
+  const float uh = planar1_uh(u, w, __builtin_amdgcn_rcpf(nw2), m);
+  z = fmaf(uh, tanh_fast(fmaf(w, z, b)), z);
 }
 
 __device__ __forceinline__ void radial1_z(float& z, float a0, float b0, float g) {
@@ -232,7 +231,7 @@ __device__ __forceinline__ void planar1_bwd(float z, float& a, float p0, float p
   const float rn = __builtin_amdgcn_rcpf(nw2);
   const float q0 = c * rn;
   const float cn = fmaf(fmaf(-nw2, q0, c), rn, q0);  // c / n, Newton-refined
-  const float uh = planar1_uh(u, w, nw2, rn, m);     // (planar1_fast's well-conditioned form)
+  const float uh = planar1_uh(u, w, rn, m);  // (planar1_fast's well-conditioned form)
   const float s = fmaf(w, z, p2);
   const float E = __builtin_amdgcn_exp2f(fabsf(s) * (-2.0f * kLog2e));
   const float rE = __builtin_amdgcn_rcpf(1.0f + E);

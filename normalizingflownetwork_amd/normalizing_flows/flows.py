@@ -6,7 +6,8 @@ wrong parameter width, static ``get_param_size(n_dims)``, and the bijector
 methods ``forward`` / ``_forward`` / ``forward_log_det_jacobian`` /
 ``_forward_log_det_jacobian``.  The parameter constraints (``_u_circ``,
 ``_alpha_circ``, ``_beta_circ``) are applied inside the HIP kernel
-(``csrc/nfn_kernels.hip``: ``planar_step`` / ``radial_step`` / ``affine_step``),
+(``csrc/nfn_device.h``: ``planar_step`` / ``radial_step`` / ``affine_step``, launched by
+``csrc/nfn_tile.hip``'s ``flow_fwd_ldj_kernel``),
 so a flow object only holds its raw parameter tensor ``t`` on the device.
 
 Inputs may be torch tensors (any device), numpy arrays or nested lists; they

@@ -58,11 +58,13 @@ def record_parity(what, got, ref64, ref32, err, bound, kind="forward"):
     widening, their count and max |gpu - ref64| / |ref32 - ref64|; the worst sample
     relative to its bound.  ``bound`` is the check's own per-element tolerance (forward:
     oracle.tolerance_bound; backward: nfn_grad_oracle.grad_tolerance)."""
-    got = np.asarray(got, np.float64).ravel()
-    ref64 = np.asarray(ref64, np.float64).ravel()
-    ref32 = np.asarray(ref32, np.float64).ravel()
-    err = np.asarray(err, np.float64).ravel()
-    bound = np.broadcast_to(np.asarray(bound, np.float64), err.shape).ravel()
+    err = np.asarray(err, np.float64)
+    shape = err.shape
+    bound = np.broadcast_to(np.asarray(bound, np.float64), shape).ravel()
+    got = np.broadcast_to(np.asarray(got, np.float64), shape).ravel()
+    ref64 = np.broadcast_to(np.asarray(ref64, np.float64), shape).ravel()
+    ref32 = np.broadcast_to(np.asarray(ref32, np.float64), shape).ravel()
+    err = err.ravel()
     dev32 = np.abs(ref32 - ref64)
     base = 1e-5 * np.maximum(1.0, np.abs(ref64))
     fin = np.isfinite(ref64) & np.isfinite(got)

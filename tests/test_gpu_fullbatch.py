@@ -12,6 +12,7 @@ every non-finite one must be non-finite on the GPU too (``tests/parity.py``).  T
   one GPU (t is 8.6 GB) (``BayesianNNEstimator.py:65-76``, ``scorers.py:13-27``)
 """
 
+import os
 import time
 from concurrent.futures import ThreadPoolExecutor
 
@@ -26,6 +27,20 @@ pytestmark = pytest.mark.gpu
 
 CHUNK = 1 << 20
 THREADS = 8
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _dump_worst(name, got, r64, r32, rows, n=256):
+    """The n samples with the largest error / bound, with their input rows (the evidence
+    for profiles/ and for tools/eval_rows.py, which replays them through any library build)."""
+    with np.errstate(all="ignore"):
+        ratio = np.abs(got - r64) / O.tolerance_bound(r64, r32)
+    ratio = np.where(np.isfinite(ratio), ratio, -1.0)
+    idx = np.argsort(ratio)[::-1][:n]
+    out = os.path.join(REPO, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    np.savez_compressed(os.path.join(out, f"fullbatch_{name}_worst.npz"), idx=idx, got=got[idx], ref64=r64[idx],
+                        ref32=r32[idx], ratio=ratio[idx], **{k: v(idx) for k, v in rows.items()})
 
 
 def _chunked(fn, n, chunk=CHUNK):
@@ -59,6 +74,7 @@ def test_full_batch_parity(cfg, gpu):
                     O.chain_log_prob(yh[lo:hi], th[lo:hi], ft, d, True, np.float32))
 
     r64, r32 = _chunked(ref, B)
+    _dump_worst(cfg, got, r64, r32, {"y": lambda i: yh[i], "t": lambda i: th[i]})
     m = check_forward(got, r64, r32, f"{cfg} full batch (B={B})", nonfinite="match", kind="full_batch")
     print(f"  {cfg}: max |err| / max(1, |ref|) = {m:.3g}", flush=True)
     fin = np.isfinite(got)
@@ -93,6 +109,8 @@ def test_c5_global_posterior_parity(gpu):
                     O.posterior_lse(yh[lo:hi], tc, ft, 1, True, dtype=np.float32))
 
     r64, r32 = _chunked(ref, B, chunk)
+    _dump_worst("C5", got, r64, r32, {"y": lambda i: yh[i],
+                                      "t": lambda i: np.stack([th[j // chunk][:, j % chunk] for j in i], axis=1)})
     m = check_forward(got, r64, r32, f"C5 global posterior (S={S}, B={B})", nonfinite="match", kind="full_batch")
     print(f"  C5: max |err| / max(1, |ref|) = {m:.3g}", flush=True)
     if np.isfinite(got).all():
