@@ -51,13 +51,15 @@ PARITY = []
 WIDEN_CAP = 2.0
 
 
-def record_parity(what, got, ref64, ref32, err, bound, kind="forward"):
+def record_parity(what, got, ref64, ref32, err, bound, kind="forward", sens32=None, n_sens=0):
     """Per check: the max of |gpu - ref64| / max(1, |ref64|); the max of |gpu - ref64| / |ref64|
     over |ref64| < 1 and how many samples there pass only through the max(1, |ref|) floor
     (err > 1e-5 |ref| but <= 1e-5); the samples admitted only through the fp32-conditioning
     widening, their count and max |gpu - ref64| / |ref32 - ref64|; the worst sample
-    relative to its bound.  ``bound`` is the check's own per-element tolerance (forward:
-    oracle.tolerance_bound; backward: nfn_grad_oracle.grad_tolerance)."""
+    relative to its bound; the reference fp32 mirror's own error statistics on the same
+    samples (how many exceed 1e-5, its largest relative error).  ``bound`` is the check's
+    own per-element tolerance (tests/parity.py); ``sens32`` the fp32 sensitivity it used
+    (``n_sens`` samples measured with input perturbations)."""
     err = np.asarray(err, np.float64)
     shape = err.shape
     bound = np.broadcast_to(np.asarray(bound, np.float64), shape).ravel()
@@ -65,7 +67,9 @@ def record_parity(what, got, ref64, ref32, err, bound, kind="forward"):
     ref64 = np.broadcast_to(np.asarray(ref64, np.float64), shape).ravel()
     ref32 = np.broadcast_to(np.asarray(ref32, np.float64), shape).ravel()
     err = err.ravel()
-    dev32 = np.abs(ref32 - ref64)
+    sens = None if sens32 is None else np.broadcast_to(np.asarray(sens32, np.float64), shape).ravel()
+    with np.errstate(invalid="ignore"):
+        dev32 = np.abs(ref32 - ref64)
     base = 1e-5 * np.maximum(1.0, np.abs(ref64))
     fin = np.isfinite(ref64) & np.isfinite(got)
     small = fin & (np.abs(ref64) < 1.0) & (ref64 != 0.0)
@@ -87,6 +91,12 @@ def record_parity(what, got, ref64, ref32, err, bound, kind="forward"):
         "widened_max_err_over_dev32": float((err[widened] / np.maximum(dev32[widened], 1e-300)).max())
         if widened.any() else None,
         "widened_max_err_over_base": float((err[widened] / base[widened]).max()) if widened.any() else None,
+        "widened_max_err_over_sens32": float((err[widened] / np.maximum(sens[widened], 1e-300)).max())
+        if (widened.any() and sens is not None) else None,
+        "n_sens_measured": int(n_sens),
+        "ref32_n_over_base": int((fin & (dev32 > base)).sum()),
+        "ref32_max_err_over_max1ref": float((dev32[fin] / np.maximum(1.0, np.abs(ref64[fin]))).max())
+        if fin.any() else None,
         "worst": {"idx": w, "got": float(got[w]), "ref64": float(ref64[w]), "ref32": float(ref32[w]),
                   "err_over_bound": float(err[w] / bound[w])} if err.size else None,
     })

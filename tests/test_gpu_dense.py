@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from oracle import nfn_oracle as O
-from parity import check_bound, check_forward, check_grad
+from parity import check_bound, check_forward, check_grad, fp32_sensitivity
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +46,8 @@ def test_dense_matches_oracle(math_mode, ft, d, H, B):
     ref64 = O.chain_log_prob(y, t64, ft, d, True, np.float64)
     ref32 = O.chain_log_prob(y, t32, ft, d, True, np.float32)
     got = out.cpu().numpy()
-    check_forward(got, ref64, ref32, f"dense {ft[:2]}x{len(ft)} d={d} H={H} B={B} [{math_mode}]", kind="dense")
+    check_forward(got, ref64, ref32, f"dense {ft[:2]}x{len(ft)} d={d} H={H} B={B} [{math_mode}]", kind="dense",
+                  sensitivity=fp32_sensitivity(y, t32, ft, d, True))
     bound = O.tolerance_bound(ref64, ref32)
     assert abs(s.item() - ref64.sum()) <= bound.sum() + 1e-6 * abs(ref64.sum())
 
@@ -189,7 +190,7 @@ def test_dense_grad_matches_oracle(math_mode, ft, d, H, B):
     ref64 = O.chain_log_prob(y, t64, ft, d, True, np.float64)
     ref32 = O.chain_log_prob(y, t32, ft, d, True, np.float32)
     check_forward(lp.cpu().numpy(), ref64, ref32, f"dense grad log_prob {ft[:2]}x{len(ft)} d={d} H={H} [{math_mode}]",
-                  kind="dense_grad")
+                  kind="dense_grad", sensitivity=fp32_sensitivity(y, t32, ft, d, True))
     # deterministic: a second run is bitwise identical
     _, gh2, gW2, gb2, _ = ops.chain_log_prob_dense_grad(torch.from_numpy(y).cuda(), torch.from_numpy(h).cuda(),
                                                          torch.from_numpy(W).cuda(), torch.from_numpy(b).cuda(), ft,
@@ -276,5 +277,6 @@ def test_dense1_grad_kernel_shapes(gpu, ft, H, B, trainable, g_none):
     t64 = h64 @ W64 + b.astype(np.float64)
     ref64 = O.chain_log_prob(z, t64, ft, d, trainable, np.float64) - np.log(2.0)
     ref32 = O.chain_log_prob(z, t32, ft, d, trainable, np.float32) - np.float32(np.log(2.0))
+    sens = fp32_sensitivity(z, t32, ft, d, trainable)
     check_forward(lp.cpu().numpy(), ref64, ref32, f"dense1 grad log_prob {ft[:2]}x{len(ft)} H={H} B={B}",
-                  kind="dense_grad")
+                  kind="dense_grad", sensitivity=sens)

@@ -21,7 +21,7 @@ import pytest
 import torch
 
 from oracle import nfn_oracle as O
-from parity import check_forward
+from parity import check_forward, fp32_sensitivity
 
 pytestmark = pytest.mark.gpu
 
@@ -75,7 +75,8 @@ def test_full_batch_parity(cfg, gpu):
 
     r64, r32 = _chunked(ref, B)
     _dump_worst(cfg, got, r64, r32, {"y": lambda i: yh[i], "t": lambda i: th[i]})
-    m = check_forward(got, r64, r32, f"{cfg} full batch (B={B})", nonfinite="match", kind="full_batch")
+    m = check_forward(got, r64, r32, f"{cfg} full batch (B={B})", nonfinite="match", kind="full_batch",
+                      sensitivity=fp32_sensitivity(yh, th, ft, d, True))
     print(f"  {cfg}: max |err| / max(1, |ref|) = {m:.3g}", flush=True)
     fin = np.isfinite(got)
     if fin.all():
@@ -111,7 +112,12 @@ def test_c5_global_posterior_parity(gpu):
     r64, r32 = _chunked(ref, B, chunk)
     _dump_worst("C5", got, r64, r32, {"y": lambda i: yh[i],
                                       "t": lambda i: np.stack([th[j // chunk][:, j % chunk] for j in i], axis=1)})
-    m = check_forward(got, r64, r32, f"C5 global posterior (S={S}, B={B})", nonfinite="match", kind="full_batch")
+    def sens(idx):
+        tt = np.stack([th[j // chunk][:, j % chunk] for j in idx], axis=1)
+        return fp32_sensitivity(yh[idx], tt, ft, 1, True, posterior=True)(np.arange(len(idx)))
+
+    m = check_forward(got, r64, r32, f"C5 global posterior (S={S}, B={B})", nonfinite="match", kind="full_batch",
+                      sensitivity=sens)
     print(f"  C5: max |err| / max(1, |ref|) = {m:.3g}", flush=True)
     if np.isfinite(got).all():
         assert float(s.item()) == pytest.approx(got.astype(np.float64).sum(), rel=1e-12)

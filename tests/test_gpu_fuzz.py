@@ -9,7 +9,7 @@ import torch
 
 from oracle import nfn_grad_oracle as G
 from oracle import nfn_oracle as O
-from parity import check_forward, check_grad
+from parity import check_forward, check_grad, fp32_sensitivity
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +46,7 @@ def test_random_chain(seed, gpu):
     bound = O.tolerance_bound(ref64, ref32)
     ok = np.isfinite(ref64)
     check_forward(lp.cpu().numpy(), ref64, ref32, f"fuzz {seed} forward d={d} K={len(ft)} B={B}", nonfinite="match",
-                  kind="fuzz")
+                  kind="fuzz", sensitivity=fp32_sensitivity(y, t, ft, d, tr))
     assert abs(s.item() - ref64[ok].sum()) <= bound[ok].sum() + 1e-6 * abs(ref64[ok].sum()) or not ok.all()
     # backward
     nb = min(B, 300)

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from conftest import CHAIN_FIXTURES, load_golden
-from parity import check_forward, check_grad
+from parity import check_forward, check_grad, fp32_sensitivity
 from oracle import nfn_grad_oracle as G
 
 pytestmark = pytest.mark.gpu
@@ -60,7 +60,8 @@ def test_grad_fixture_vs_oracle(gpu, math_mode, name):
     # the backward's own log_prob equals the forward oracle
     from oracle import nfn_oracle as O
 
-    check_forward(lp, fx["ref64"][:B], fx["ref32"][:B], f"{name} backward's log_prob [{math_mode}]", nonfinite="match")
+    check_forward(lp, fx["ref64"][:B], fx["ref32"][:B], f"{name} backward's log_prob [{math_mode}]", nonfinite="match",
+                  sensitivity=fp32_sensitivity(y, t, ft, d, tr))
 
 
 @pytest.mark.parametrize("ft,d", [(("planar", "radial") * 5, 1), (("affine", "planar", "radial"), 3),

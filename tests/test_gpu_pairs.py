@@ -14,7 +14,7 @@ import torch
 
 from oracle import nfn_grad_oracle as G
 from oracle import nfn_oracle as O
-from parity import check_forward, check_grad
+from parity import check_forward, check_grad, fp32_sensitivity
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +46,8 @@ def test_pair_form_forward_and_posterior(ft, gpu):
     with np.errstate(all="ignore"):
         r64 = O.chain_log_prob(y, t, ft, 1, True, np.float64)
         r32 = O.chain_log_prob(y, t, ft, 1, True, np.float32)
-    check_forward(lp.cpu().numpy(), r64, r32, f"pairs {_ids(ft)} forward", nonfinite="match")
+    check_forward(lp.cpu().numpy(), r64, r32, f"pairs {_ids(ft)} forward", nonfinite="match",
+                  sensitivity=fp32_sensitivity(y, t, ft, 1, True))
     # posterior: S draws of t per sample
     S, Bp = 3, 333
     tp = (0.7 * rng.standard_normal((S, Bp, P))).astype(np.float32)
@@ -75,7 +76,8 @@ def test_pair_form_backward(ft, gpu):
     with np.errstate(all="ignore"):
         r64 = O.chain_log_prob(y, t, ft, 1, True, np.float64)
         r32 = O.chain_log_prob(y, t, ft, 1, True, np.float32)
-    check_forward(lp.cpu().numpy(), r64, r32, f"pairs {_ids(ft)} backward's log_prob", nonfinite="match")
+    check_forward(lp.cpu().numpy(), r64, r32, f"pairs {_ids(ft)} backward's log_prob", nonfinite="match",
+                  sensitivity=fp32_sensitivity(y, t, ft, 1, True))
 
 
 @pytest.mark.parametrize("ft", [("planar", "radial") * 5, ("affine",) * 15, ("planar", "radial", "planar", "affine", "radial")],

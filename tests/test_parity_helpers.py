@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import conftest
-from parity import check_bound, check_forward, check_grad
+from parity import check_bound, check_forward, check_grad, fp32_sensitivity
 
 
 @pytest.fixture(autouse=True)
@@ -60,3 +60,29 @@ def test_check_grad_and_bound_2d():
     check_bound(ref[0] + 5e-6, ref[0], 1e-5, "scalar bound", kind="dense_grad")
     with pytest.raises(AssertionError):
         check_bound(ref + 2e-5, ref, bound, "out of bound", kind="dense_grad")
+
+
+def test_check_forward_with_measured_sensitivity():
+    """A sample beyond the base bound is judged against the reference's fp32 sensitivity
+    measured with input perturbations (only for the samples that need it)."""
+    ft = ("planar", "radial") * 5
+    g = conftest.load_golden("stress_pr5_d1")
+    y, t, r64, r32 = g["y"][:512], g["t"][:512], g["ref64"][:512], g["ref32"][:512]
+    calls = []
+    sens = fp32_sensitivity(y, t, ft, 1, True)
+
+    def counting(idx):
+        calls.append(len(idx))
+        return sens(idx)
+
+    check_forward(r64.copy(), r64, r32, "exact", sensitivity=counting)
+    assert calls == []  # nothing beyond the base bound: no oracle re-runs
+    dev = np.abs(r32 - r64) / np.maximum(1.0, np.abs(r64))
+    i = int(np.argmax(dev))
+    s_i = float(sens(np.array([i]))[0])  # the same perturbations check_forward draws for this one sample
+    got = r64.copy()
+    got[i] += 1.5 * s_i  # within 2x the measured sensitivity
+    if 1.5 * s_i > 1e-5 * max(1.0, abs(r64[i])):
+        check_forward(got, r64, r32, "within sensitivity", sensitivity=counting)
+        assert calls == [1]
+        assert conftest.PARITY[-1]["n_sens_measured"] == 1
