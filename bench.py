@@ -269,13 +269,14 @@ def main():
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
-    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad", "bijector"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad", "bijector", "flows"],
                     help="forward = fused log_prob (the headline); grad = the fused backward of the "
                          "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient); dense = the "
                          "output Dense layer (H -> P) fused into the chain, streaming h instead of t; "
                          "dense_grad = the training step's backward through that fused layer (dh, dW, db, dy); "
                          "bijector = the Bijector API's Chain.forward + forward_log_det_jacobian over the "
-                         "layer's flows in one launch (no base density)")
+                         "layer's flows in one launch (no base density); flows = the same Chain flow by flow, "
+                         "one single-flow launch per flow (nfn_flow_fwd_ldj_f32)")
     ap.add_argument("--hidden", type=int, default=16, help="--mode dense / dense_grad: hidden width H")
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the all-reduce even at N = 1 (tests)")
@@ -324,10 +325,10 @@ def main():
             launcher = ops.DenseGradLauncher(y, h, Wd, bd, ft, d, True, g_out=g_up)
         else:
             launcher = (ops.DenseLauncher if S is None else ops.PosteriorDenseLauncher)(y, h, Wd, bd, ft, d, True)
-    elif args.mode == "bijector":
-        assert S is None, "--mode bijector covers the plain chain configs (C2, C3)"
+    elif args.mode in ("bijector", "flows"):
+        assert S is None, "--mode bijector / flows cover the plain chain configs (C2, C3)"
         t = torch.randn((B, P), generator=gen, device=dev)
-        launcher = ops.BijectorLauncher(y, t, ft, d, True)
+        launcher = (ops.BijectorLauncher if args.mode == "bijector" else ops.FlowsLauncher)(y, t, ft, d, True)
     else:
         t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
         if grad_mode:
@@ -367,7 +368,7 @@ def main():
         launcher.launch(sh)
         if ev1 is not None:
             ev1.record(stream)
-        if grad_mode or args.mode == "bijector":  # per-sample outputs stay on their rank
+        if grad_mode or args.mode in ("bijector", "flows"):  # per-sample outputs stay on their rank
             return
         if direct:
             works[i] = dist.all_reduce(reds[i], async_op=True)
@@ -495,7 +496,7 @@ def main():
         if dense_mode:
             del t_buf, plain
     nonfinite = None
-    if grad_mode or args.mode == "bijector":
+    if grad_mode or args.mode in ("bijector", "flows"):
         mean_ll = None
     elif native is not None:
         mean_ll = float(native.mean.item())
@@ -519,6 +520,9 @@ def main():
         elif args.mode == "bijector":
             # z in, the flows' blocks of t (P - 2d floats), z_K and ldj out
             bytes_launch = float(B) * (4 * d + 4 * (P - 2 * d) + 4 * d + 4)
+        elif args.mode == "flows":
+            # per flow: z in, its block of t, z and its ldj out (the K launches of one step)
+            bytes_launch = launcher.bytes_per_launch
         elif args.mode == "dense_grad":
             # h, y, upstream g in; dh, dy out; W, b read and dW, db written once per launch
             bytes_launch = float(B) * (8 * H + 8 * d + 4) + 2 * (4.0 * H * P + 4.0 * P)
@@ -526,10 +530,11 @@ def main():
             bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense", "dense_grad": "_dense_grad",
-                                                           "bijector": "_bijector"}.get(args.mode, ""), B)
+                                                           "bijector": "_bijector", "flows": "_flows"}.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.mode, args.config, H=H, seconds=args.cpu_seconds)
+            cpu = cpu_baseline("bijector" if args.mode == "flows" else args.mode, args.config, H=H,
+                               seconds=args.cpu_seconds)
         wl = {
             "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
             "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
@@ -545,6 +550,9 @@ def main():
         elif args.mode == "bijector":
             kernel_name = "chain_wave1_kernel (Chain bijector form)" if d == 1 else "chain_fwd_ldj_kernel"
             metric = f"Chain bijector forward+fldj evals/sec (whole node), {args.config}"
+        elif args.mode == "flows":
+            kernel_name = f"flow_fwd_ldj_kernel x {len(ft)} launches"
+            metric = f"flow-by-flow bijector forward+fldj chain evals/sec (whole node), {args.config}"
         elif args.mode == "dense":
             if S is None:
                 kernel_name = "chain_dense1_kernel" if d == 1 else "chain_dense_kernel"

@@ -1893,6 +1893,22 @@ __global__ void __launch_bounds__(kMaxBlock)
                         float* __restrict__ z_out, float* __restrict__ ldj_out) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  if constexpr (DM == 1 && FAST) {
+    // d = 1: the chain kernels' d = 1 bijectors on the block's 2-3 floats, loaded
+    // non-temporally (each launch reads every row's 128-B line of t once: a 12-B span of a
+    // line costs a whole-line fetch, tools/sector_probe.hip; the default policy streams
+    // 7 % slower there)
+    const float* p = tk + b * t_rowstride;
+    float pv[3];
+    pv[0] = __builtin_nontemporal_load(p);
+    pv[1] = __builtin_nontemporal_load(p + 1);
+    pv[2] = flow_id == NFN_FLOW_AFFINE ? 0.0f : __builtin_nontemporal_load(p + 2);
+    float z1 = z_in[b * z_bstride];
+    const float det = flow1_fast(flow_id, z1, pv);
+    if (z_out) __builtin_nontemporal_store(z1, z_out + b);
+    if (ldj_out) __builtin_nontemporal_store(__builtin_amdgcn_logf(fabsf(det)) * kLn2, ldj_out + b);
+    return;
+  }
   float z[DM];
   const float* zr = z_in + b * z_bstride;
 #pragma unroll

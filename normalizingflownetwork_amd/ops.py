@@ -740,6 +740,47 @@ class BijectorLauncher:
             _lib.check(rc, "nfn_chain_fwd_ldj_f32")
 
 
+class FlowsLauncher:
+    """Pre-bound flow-by-flow Bijector path for the benchmark: the Chain's K flows as K
+    single-flow launches (``nfn_flow_fwd_ldj_f32``, PlanarFlow.py:68-80 / RadialFlow.py:50-70 /
+    AffineFlow.py called one bijector at a time), each reading its own block of every row
+    of ``t`` (the layer's reversed layout) and the previous flow's z, writing z and its own
+    log|det J| (``ldj`` (K, B)).  ``z_out`` holds z_K after ``launch()``."""
+
+    def __init__(self, z: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
+                 trainable_base: bool):
+        self.lib = _lib.load()
+        dev = z.device
+        d = int(n_dims)
+        P = total_param_size(flow_types, d, trainable_base)
+        assert z.dim() == 2 and z.shape[1] == d and z.stride(1) == 1
+        assert t.dim() == 2 and t.shape[1] == P and t.stride(1) == 1
+        B = max(int(z.shape[0]), int(t.shape[0]))
+        self.B, K = B, len(flow_types)
+        off, offs = 2 * d if trainable_base else 0, [0] * K
+        for k in reversed(range(K)):
+            offs[k] = off
+            off += param_size(flow_types[k], d)
+        zs = [torch.empty((B, d), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.ldj = torch.empty((max(1, K), B), dtype=torch.float32, device=dev)
+        self.z_out = zs[(K - 1) % 2] if K else z
+        self._calls = []
+        zin = z
+        for k, f in enumerate(flow_types):
+            zo = zs[k % 2]
+            self._calls.append((FLOW_IDS[f], _ptr(zin), _row_stride(zin), _ptr(t) + 4 * offs[k], _row_stride(t), B, d,
+                                _ptr(zo), _ptr(self.ldj[k])))
+            zin = zo
+        self.bytes_per_launch = float(B) * sum(4 * d + 4 * param_size(f, d) + 4 * d + 4 for f in flow_types)
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        st = stream if stream is not None else _stream()
+        for args in self._calls:
+            rc = self.lib.nfn_flow_fwd_ldj_f32(*args, st)
+            if rc != 0:
+                _lib.check(rc, "nfn_flow_fwd_ldj_f32")
+
+
 class ChainLauncher:
     """Pre-bound fused-chain launch for repeated evaluation of fixed device
     buffers (the benchmark / serving loop): all validation and pointer

@@ -22,7 +22,7 @@ from oracle import nfn_grad_oracle as G
 from oracle import nfn_oracle as O
 
 
-def fp32_sensitivity(y, t, flow_types, d, trainable, y_mean=None, y_std=None, n_perturbed=16, posterior=False):
+def fp32_sensitivity(y, t, flow_types, d, trainable, y_mean=None, y_std=None, n_perturbed=64, posterior=False):
     """``idx -> S32[idx]``: the reference's own fp32 sensitivity on those samples, the
     largest deviation from the fp64 truth of the oracle's op-by-op fp32 mirror evaluated
     at the inputs and at ``n_perturbed`` copies moved by one random ulp
@@ -65,7 +65,7 @@ def check_forward(got, ref64, ref32, what, extra_rel: float = 0.0, nonfinite: st
         |gpu - ref64| <= max(1e-5 * max(1, |ref64|), WIDEN_CAP * S32)
     with S32 the reference's own fp32 deviation on the sample: |ref32 - ref64| of the
     oracle's op-by-op fp32 run, or — when the check has its inputs (``sensitivity``, from
-    :func:`fp32_sensitivity`) — the largest such deviation over that run and 16 runs at
+    :func:`fp32_sensitivity`) — the largest such deviation over that run and 64 runs at
     1-ulp perturbations of the inputs (one fp32 evaluation order can be luckily accurate
     on an ill-conditioned sample; the OCML-precise build of these kernels misses the
     single-run form on the same samples, DESIGN.md "Tolerances").

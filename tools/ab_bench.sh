@@ -8,7 +8,7 @@ TAG=$1; CFGS=$2; shift 2
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-for r in 1 2 3; do
+for r in $(seq 1 ${REPS:-3}); do
   for cfg in $CFGS; do
     for v in "$@"; do
       dir=$ROOT/_ab/$v; [ "$v" = cur ] && dir=$ROOT
