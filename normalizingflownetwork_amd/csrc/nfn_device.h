@@ -1169,7 +1169,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
 // FWD: the Bijector API's Chain forward + forward_log_det_jacobian instead of log_prob
 // (nfn_chain_fwd_ldj_f32 over the layer's flow blocks; needs FAST and PACKED): z_K goes to
 // a.z_out and sum_k log|det J_k| to a.out; no base density, no partial sums.
-template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop>
+// DMA (diagnostic A/B, NFN_DIAG builds: NFN_WAVE1_DMA=1): the tile's rows go global -> LDS
+// by LDS-DMA (buffer_load_dword ... lds, non-temporal), one instruction per row (the
+// row's P dwords, lanes 0..P-1) so the odd row stride and every read stay as they are,
+// into the other of two LDS slots per wave while the chain reads the current one; no
+// register prefetch, no ds_write hand-off.  The next hand-off waits with an explicit
+// vmcnt(1) (hipcc does not order a ds_read behind an LDS-DMA).
+template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop, bool DMA = false>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
@@ -1180,7 +1186,8 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   const int S = a.lds_stride;
   const int64_t rs = a.t_rowstride;
   const int r0 = lane / Q, c4 = lane % Q;
-  float* tl = lds + wid * 64 * S;
+  float* tl = lds + wid * 64 * S * (DMA ? 2 : 1);
+  float* tl_next = tl + 64 * S;  // DMA: the slot the next tile lands in
   const int l0 = r0 * S + 4 * c4;
   const int64_t ntiles = a.ntiles;
   const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -1202,7 +1209,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   // Tiles past the end are issued too, through empty descriptors (no memory traffic,
   // zeros returned): every path then holds the same loads in the same order and the
   // waitcnt pass counts each hand-off's wait exactly.
-  float4 buf[Q];
+  float4 buf[DMA ? 1 : Q];
   float ybuf;
   auto issue = [&](int64_t tile) {
     if (abl_tile >= 0) tile = abl_tile;
@@ -1210,11 +1217,22 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     const int64_t b0c = nr > 0 ? b0 : 0;
     const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
-    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
     const auto rt = tile_rsrc(a.t + b0c * rs, nr > 0 ? ((nr - 1) * rs + a.P) * 4 : 0);
+    if constexpr (DMA) {
+      // rows first, y last: the hand-off's wait for y (and its vmcnt(1)) covers them
+      if (lane < 4 * Q) {
 #pragma unroll
-    for (int k = 0; k < Q; ++k)
-      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+        for (int r = 0; r < 64; ++r)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(tl_next + r * S), 4,
+                                                   lane * 4, r * (int)rs * 4, 0, kNT);
+      }
+      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    } else {
+      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+#pragma unroll
+      for (int k = 0; k < Q; ++k)
+        buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+    }
   };
 
   double acc = 0.0;
@@ -1235,13 +1253,26 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
+    if constexpr (DMA) {
+      // this tile's rows (issued before its y) have landed; only the last store may be
+      // outstanding.  Then the slots swap: the chain reads what just landed, the next
+      // tile's rows go to the slot the previous chain finished reading (wave_lds_sync)
+      if constexpr (FWD)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // flush() issues two stores
+      else
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      float* const t_ = tl;
+      tl = tl_next;
+      tl_next = t_;
+    } else {
 #pragma unroll
-    for (int k = 0; k < Q; ++k) {
-      float* dst = tl + l0 + k * RSTEP * S;
-      dst[0] = buf[k].x;
-      dst[1] = buf[k].y;
-      dst[2] = buf[k].z;
-      dst[3] = buf[k].w;
+      for (int k = 0; k < Q; ++k) {
+        float* dst = tl + l0 + k * RSTEP * S;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
     }
     const float z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
     wave_lds_sync();
@@ -1881,45 +1912,6 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   if (a.partials) {
     write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
   }
-}
-
-// Single bijector over a batch (the per-flow Bijector API).  Parameters are read
-// straight from global memory: this path serves the Python Bijector objects,
-// not the fused chain.
-template <int DM, bool FAST>
-__global__ void __launch_bounds__(kMaxBlock)
-    flow_fwd_ldj_kernel(int32_t flow_id, const float* __restrict__ z_in, int64_t z_bstride,
-                        const float* __restrict__ tk, int64_t t_rowstride, int64_t B, int32_t d,
-                        float* __restrict__ z_out, float* __restrict__ ldj_out) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  if constexpr (DM == 1 && FAST) {
-    // d = 1: the chain kernels' d = 1 bijectors on the block's 2-3 floats, loaded
-    // non-temporally (each launch reads every row's 128-B line of t once: a 12-B span of a
-    // line costs a whole-line fetch, tools/sector_probe.hip; the default policy streams
-    // 7 % slower there)
-    const float* p = tk + b * t_rowstride;
-    float pv[3];
-    pv[0] = __builtin_nontemporal_load(p);
-    pv[1] = __builtin_nontemporal_load(p + 1);
-    pv[2] = flow_id == NFN_FLOW_AFFINE ? 0.0f : __builtin_nontemporal_load(p + 2);
-    float z1 = z_in[b * z_bstride];
-    const float det = flow1_fast(flow_id, z1, pv);
-    if (z_out) __builtin_nontemporal_store(z1, z_out + b);
-    if (ldj_out) __builtin_nontemporal_store(__builtin_amdgcn_logf(fabsf(det)) * kLn2, ldj_out + b);
-    return;
-  }
-  float z[DM];
-  const float* zr = z_in + b * z_bstride;
-#pragma unroll
-  for (int j = 0; j < DM; ++j) z[j] = (j < d) ? zr[j] : 0.0f;
-  const float ldj = flow_step<DM, FAST>(flow_id, z, tk + b * t_rowstride, d);
-  if (z_out) {
-#pragma unroll
-    for (int j = 0; j < DM; ++j)
-      if (j < d) z_out[b * d + j] = z[j];
-  }
-  if (ldj_out) ldj_out[b] = ldj;
 }
 
 }  // namespace nfn

@@ -26,6 +26,12 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
   if (cm == kChainPairs && a.prog.K <= 16) kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
   if (cm == kStaticProg && a.prog.K == kStaticK[0] && a.prog.types[0] == kStaticTypes[0])
     kfn = chain_wave1_kernel<true, Q, true, false, kStaticProg>;
+  // LDS-DMA row fill (A/B): two LDS slots per wave, d = 1 packed loop form
+  if (env_int("NFN_WAVE1_DMA", 0) == 1 && Q <= 8 && a.prog.K <= 16) {
+    kfn = a.prog.K <= kPairsMaxKStream ? chain_wave1_kernel<true, Q, true, false, kChainPairs, true>
+                                       : chain_wave1_kernel<true, Q, true, false, kChainLoop, true>;
+    lds = 2 * (lds - 16) + 16;
+  }
 #endif
 #endif
   const int64_t units = a.ntiles;

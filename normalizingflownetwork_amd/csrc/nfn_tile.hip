@@ -3,6 +3,50 @@
 #include "nfn_launch.h"
 
 namespace nfn {
+
+// Single bijector over a batch (the per-flow Bijector API).  Parameters are read
+// straight from global memory: this path serves the Python Bijector objects,
+// not the fused chain.
+template <int DM, bool FAST, int V = 1>
+__global__ void __launch_bounds__(kMaxBlock)
+    flow_fwd_ldj_kernel(int32_t flow_id, const float* __restrict__ z_in, int64_t z_bstride,
+                        const float* __restrict__ tk, int64_t t_rowstride, int64_t B, int32_t d,
+                        float* __restrict__ z_out, float* __restrict__ ldj_out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  if constexpr (DM == 1 && FAST && V != 0) {
+    // d = 1: the chain kernels' d = 1 bijectors on the block's 2-3 floats.  Each launch
+    // reads every row's 128-B line of t once — a 12-B span costs a whole-line fetch
+    // (tools/sector_probe.hip: 1-3 dwords of every row of 2^24 take as long as streaming
+    // all 2.15 GB), so ten single-flow launches at C2 are bounded by ~3.6 ms of line fetches.
+    // Default-policy loads: the block arrives as two requests (x2 + x1) to the same line,
+    // and non-temporal ones let the second refetch it (5.9 vs 4.3 ms for the ten flows,
+    // tools/microbench.py flows, profiles/r03/); z and the log-det are stored with the
+    // default policy too: the next flow's launch reads this z back.
+    const float* p = tk + b * t_rowstride;
+    float pv[3];
+    pv[0] = p[0];
+    pv[1] = p[1];
+    pv[2] = flow_id == NFN_FLOW_AFFINE ? 0.0f : p[2];
+    float z1 = z_in[b * z_bstride];
+    const float det = flow1_fast(flow_id, z1, pv);
+    if (z_out) z_out[b] = z1;
+    if (ldj_out) ldj_out[b] = __builtin_amdgcn_logf(fabsf(det)) * kLn2;
+    return;
+  }
+  float z[DM];
+  const float* zr = z_in + b * z_bstride;
+#pragma unroll
+  for (int j = 0; j < DM; ++j) z[j] = (j < d) ? zr[j] : 0.0f;
+  const float ldj = flow_step<DM, FAST>(flow_id, z, tk + b * t_rowstride, d);
+  if (z_out) {
+#pragma unroll
+    for (int j = 0; j < DM; ++j)
+      if (j < d) z_out[b * d + j] = z[j];
+  }
+  if (ldj_out) ldj_out[b] = ldj;
+}
+
 namespace {
 
 // The Bijector API's Chain (tfp Chain of the flows that InverseNormalizingFlowLayer.
@@ -84,8 +128,9 @@ template <int DM, bool FAST>
 void launch_f(int32_t flow_id, const float* z, int64_t zs, const float* tk, int64_t ts, int64_t B, int32_t d,
               float* z_out, float* ldj_out, hipStream_t s) {
   const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
-  hipLaunchKernelGGL((flow_fwd_ldj_kernel<DM, FAST>), dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, flow_id, z, zs,
-                     tk, ts, B, d, z_out, ldj_out);
+  // NFN_FLOW_VARIANT=0 (diag A/B): the generic bijector code for d = 1 too
+  auto k = env_int("NFN_FLOW_VARIANT", 1) == 0 ? flow_fwd_ldj_kernel<DM, FAST, 0> : flow_fwd_ldj_kernel<DM, FAST, 1>;
+  hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, flow_id, z, zs, tk, ts, B, d, z_out, ldj_out);
 }
 
 template <bool FAST>

@@ -475,6 +475,60 @@ def main():
     if which[0] == "pdense":
         run_posterior_dense()
         return
+    if which[0] == "flows":  # the per-flow Bijector path at C2: d = 1 fast-path kernel vs the generic one
+        ft, d, B, _ = CFG["C2"]
+        P = ops.total_param_size(ft, d, True)
+        gen = torch.Generator(device="cuda").manual_seed(1)
+        y = torch.randn((B, d), generator=gen, device="cuda")
+        t = torch.randn((B, P), generator=gen, device="cuda")
+        L = ops.FlowsLauncher(y, t, ft, d, True)
+        stream = torch.cuda.current_stream()
+        sh = int(stream.cuda_stream)
+        prewarm(lambda: L.launch(sh))
+        names = (("d1", {}), ("generic", {"NFN_FLOW_VARIANT": "0"}))
+        times, outs = {n: [] for n, _ in names}, {}
+        for r in range(4):
+            for name, env in names:
+                os.environ.update(env)
+                for _ in range(2):
+                    L.launch(sh)
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+                for e0, e1 in evs:
+                    e0.record(stream)
+                    L.launch(sh)
+                    e1.record(stream)
+                torch.cuda.synchronize()
+                times[name].append(float(np.median([a.elapsed_time(b) for a, b in evs])))
+                outs[name] = (L.z_out.clone(), L.ldj.clone())
+                for k in env:
+                    os.environ.pop(k)
+        ref_ldj = outs["d1"][1]
+        for name in times:
+            bad = (outs[name][1] != ref_ldj)
+            per_flow = bad.sum(dim=1).tolist()
+            first = torch.nonzero(bad[0]).flatten()[:8].tolist() if bad[0].any() else []
+            print(json.dumps({"variant": name, "mismatching_rows_per_flow": per_flow, "first_rows_flow0": first,
+                              "ldj_flow0_first": outs[name][1][0][first].tolist() if first else [],
+                              "ref_flow0_first": ref_ldj[0][first].tolist() if first else []}), flush=True)
+        for name in times:
+            print(json.dumps({"variant": name, "ms_10_flows": float(np.median(times[name])), "rounds": times[name],
+                              "maxdiff_z_vs_d1": maxdiff(outs[name][0], outs["d1"][0]),
+                              "maxdiff_ldj_vs_d1": maxdiff(outs[name][1], outs["d1"][1])}), flush=True)
+        return
+    if which[0] == "gradshape":  # the fused backward: persistent wave tiles vs one tile per workgroup
+        for cfg in ("C2",):
+            run_grad(cfg, [{"name": "wave_persistent", "env": {}},
+                           {"name": "tile_per_workgroup", "env": {"NFN_GRAD_WAVE": 0}},
+                           {"name": "wave_wpb1", "env": {"NFN_GRAD_WPB": 1}},
+                           {"name": "wave_wpb4", "env": {"NFN_GRAD_WPB": 4}}])
+        return
+    if which[0] == "dma":  # C2 forward: register prefetch + ds_write hand-off vs LDS-DMA row fill
+        for cfg in ("C2", "C1"):
+            run(cfg, [{"name": "regs", "env": {}}, {"name": "lds_dma", "env": {"NFN_WAVE1_DMA": 1}},
+                      {"name": "regs_memonly", "env": {"NFN_ABLATE_FLOWS": 1}},
+                      {"name": "lds_dma_memonly", "env": {"NFN_WAVE1_DMA": 1, "NFN_ABLATE_FLOWS": 1}}],
+                rounds=4)
+        return
     if which[0] == "ceiling":  # HBM ceilings of plain torch streams over the C2 parameter buffer
         B, P = 1 << 24, 32
         t = torch.randn((B, P), device="cuda")
