@@ -8,6 +8,7 @@ every non-finite one must be non-finite on the GPU too (``tests/parity.py``).  T
 
 * C2: d = 1, (planar, radial) x 5, B = 2^24 (``DistributionLayers.py:245-255``)
 * C3: d = 8, affine + planar x 4 + radial x 4, B = 2^22
+* C4: C2's chain at the 8-GPU global batch, B = 2^27, on one device
 * C5: the Bayesian posterior score at its GLOBAL size, S = 64 draws x B = 2^20 samples on
   one GPU (t is 8.6 GB) (``BayesianNNEstimator.py:65-76``, ``scorers.py:13-27``)
 """
@@ -53,12 +54,15 @@ def _chunked(fn, n, chunk=CHUNK):
     return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C3"])
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
 def test_full_batch_parity(cfg, gpu):
+    """C4 is C2's chain at the 8-GPU global batch (2^27) on ONE device: t is 16 GiB, the call
+    runs as eight 2^24-sample chunk launches with one fused sum (include/nfn.h)."""
     from normalizingflownetwork_amd import ops
 
     ft, d, B = {"C2": (("planar", "radial") * 5, 1, 1 << 24),
-                "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22)}[cfg]
+                "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22),
+                "C4": (("planar", "radial") * 5, 1, 1 << 27)}[cfg]
     P = O.total_param_size(ft, d, True)
     gen = torch.Generator(device="cuda").manual_seed(22)
     y = torch.randn((B, d), generator=gen, device="cuda")

@@ -515,6 +515,11 @@ def main():
                               "maxdiff_z_vs_d1": maxdiff(outs[name][0], outs["d1"][0]),
                               "maxdiff_ldj_vs_d1": maxdiff(outs[name][1], outs["d1"][1])}), flush=True)
         return
+    if which[0] == "occ":  # resident workgroups per CU for the d = 1 streaming kernels (C5 posterior, C2)
+        for cfg in ("C5", "C2"):
+            run(cfg, [{"name": "default", "env": {}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
+                      {"name": "wg4", "env": {"NFN_WG_PER_CU": 4}}], rounds=4)
+        return
     if which[0] == "gradshape":  # the fused backward: persistent wave tiles vs one tile per workgroup
         for cfg in ("C2",):
             run_grad(cfg, [{"name": "wave_persistent", "env": {}},
