@@ -249,7 +249,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradAr
 // Per wave LDS: the t tile ((P + 2) columns, the packed reverse pass reads up to two
 // past the last block) and the flow inputs z_k.  Every workgroup writes one partial
 // [dW | db], summed across waves in wave order: bitwise deterministic.
-template <int MH, int NN, int CM = kChainLoop>
+// AB (diagnostic builds only): bit 0 replaces the dh^T MFMAs, bit 1 the dW MFMAs, by a VALU
+// touch of the same operands — the ceiling any faster form of those two GEMMs could reach.
+template <int MH, int NN, int CM = kChainLoop, int AB = 0>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradArgs g) {
   const DenseArgs& da = g.da;
   const ChainArgs& a = da.c;
@@ -415,7 +417,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
         for (int mh = 0; mh < MH; ++mh) {
           f32x4v acc = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int ks = 0; ks < 4 * NN; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[mh][ks], bv[ks], acc, 0, 0, 0);
+          for (int ks = 0; ks < 4 * NN; ++ks) {
+            if constexpr (AB & 1)
+              acc[ks & 3] = fmaf(wA[mh][ks], bv[ks], acc[ks & 3]);
+            else
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[mh][ks], bv[ks], acc, 0, 0, 0);
+          }
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc), rdh, ghoff, mt * ghmt + 64 * mh, kNT);
         }
       }
@@ -433,7 +440,10 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int mh = 0; mh < MH; ++mh)
-            dw[mh][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(hA[mh][4 * kq + i], q[i], dw[mh][nt], 0, 0, 0);
+            if constexpr ((AB & 2) != 0)
+              dw[mh][nt][i] = fmaf(hA[mh][4 * kq + i], q[i], dw[mh][nt][i]);
+            else
+              dw[mh][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(hA[mh][4 * kq + i], q[i], dw[mh][nt], 0, 0, 0);
       }
     }
     wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
@@ -504,6 +514,12 @@ int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
     if (env_int("NFN_CHAIN_FORM", kChainPairs) == kStaticProg && g.da.c.prog.K == kStaticK[0] &&
         g.da.c.prog.types[0] == kStaticTypes[0])
       kfn = chain_dense1_grad_kernel<MH, NN, kStaticProg>;
+    if constexpr (MH == 1) {
+      const int ab = env_int("NFN_DGRAD_ABLATE", 0);
+      if (ab == 1) kfn = chain_dense1_grad_kernel<MH, NN, kChainPairs, 1>;
+      if (ab == 2) kfn = chain_dense1_grad_kernel<MH, NN, kChainPairs, 2>;
+      if (ab == 3) kfn = chain_dense1_grad_kernel<MH, NN, kChainPairs, 3>;
+    }
   }
 #endif
   const size_t lds = (size_t)4 * dense1_grad_wave_floats(g.da.c.P, 16 * MH + 4, g.da.c.prog.K) * sizeof(float);

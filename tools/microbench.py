@@ -235,7 +235,7 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
                           "rounds_ms": times[k]}), flush=True)
 
 
-def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False):
+def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False, gemm_ceiling=False):
     """C2 training step through the output Dense layer: the fused backward (t never
     written) vs the unfused path (library GEMM t, chain backward kernel, GEMMs for
     dh / dW and the db sum) vs the chain backward alone on a resident t."""
@@ -268,6 +268,11 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False):
     if static:
         fns = {"fused": fused, "fused_static": fused, "fused_loopform": fused}
         envs["fused_static"] = {"NFN_CHAIN_FORM": "2"}
+    if gemm_ceiling:  # dh / dW MFMAs replaced by VALU touches of the same operands (NFN_DGRAD_ABLATE)
+        fns = {"fused": fused, "no_dh_mfma": fused, "no_dW_mfma": fused, "no_dh_dW_mfma": fused,
+               "fused_gemms_only": fused}
+        envs.update({"no_dh_mfma": {"NFN_DGRAD_ABLATE": "1"}, "no_dW_mfma": {"NFN_DGRAD_ABLATE": "2"},
+                     "no_dh_dW_mfma": {"NFN_DGRAD_ABLATE": "3"}})
     os.environ["NFN_CHAIN_FORM"] = "0"
     loop_out = [x for x in fused()]
     del os.environ["NFN_CHAIN_FORM"]
@@ -471,6 +476,9 @@ def main():
         return
     if which[0] == "dgrad":
         run_dense_grad()
+        return
+    if which[0] == "dgradceil":  # what any faster dh / dW GEMM form could win at most
+        run_dense_grad(gemm_ceiling=True, rounds=4)
         return
     if which[0] == "pdense":
         run_posterior_dense()
