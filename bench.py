@@ -405,12 +405,19 @@ def main():
     # clock ramp: keep the device busy with untimed steps for >= --prewarm-ms of device time
     prewarm_steps = 0
     if args.prewarm_ms > 0:
+        # the step time is taken AFTER a first untimed step: the first launch carries the
+        # module load and first-touch costs (milliseconds), which would cut the prewarm short
+        step()
+        drain()
+        torch.cuda.synchronize()
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         pe0.record(stream)
-        step()
+        for _ in range(4):
+            step()
         pe1.record(stream)
+        drain()
         torch.cuda.synchronize()
-        per = max(pe0.elapsed_time(pe1), 1e-3)
+        per = max(pe0.elapsed_time(pe1) / 4, 1e-3)
         prewarm_steps = int(min(20000, np.ceil(args.prewarm_ms / per)))
         if dist_on:  # every rank must issue the same number of step all-reduces
             drain()

@@ -97,8 +97,8 @@ extern "C" {
 
 /* Library version as MAJOR*10000 + MINOR*100 + PATCH.
  *   200 (0.2.0): out_sum is a device double[2] {sum, non-finite count} (was double[1]);
- *                the workspace needs no initialisation (its finishing ticket is cleared on
- *                the stream by every summed call).
+ *                the workspace needs no initialisation (its finishing ticket carries a
+ *                per-call epoch).
  *   100 (0.1.0): first release. */
 #define NFN_ABI_VERSION 200
 int32_t nfn_version(void);
@@ -136,8 +136,9 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *                non-finite out_logp values}, finished inside the kernel by its last
  *                workgroup (fixed summation order: bitwise deterministic; no extra launch)
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
- *                Needs no initialisation (e.g. a plain hipMalloc): a summed call clears
- *                the ticket (workspace[1]) with a stream-ordered memset before its launch.
+ *                Needs no initialisation (e.g. a plain hipMalloc): the finishing ticket
+ *                (workspace[1]) is tagged with a per-call epoch, so a stale or garbage
+ *                ticket restarts the count (no memset launch precedes the kernel).
  *                Layout: workspace[0] = number n of per-workgroup pairs written,
  *                workspace[1] = the finishing ticket, workspace[2 + 2i] /
  *                workspace[3 + 2i] = workgroup i's fp64 partial sum / non-finite count.

@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
     wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
   }
   if (a.partials) {
-    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 
@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   }
   flush();
   if (a.partials) {
-    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 
@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
   }
   flush();
   if (a.partials) {
-    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 
@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense_kernel(DenseArgs da
     }
   }
   if (a.partials) {
-    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 

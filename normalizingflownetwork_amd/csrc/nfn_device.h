@@ -108,6 +108,7 @@ struct ChainArgs {
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
   int64_t pair_base;   // chunked batch: this launch's first partial slot (earlier chunks' pairs precede it)
+  uint32_t epoch;      // summed launch: this call's ticket epoch (non-zero, see write_partial)
   FlowProgram prog;
 };
 
@@ -819,16 +820,22 @@ __device__ __forceinline__ void sum_pairs(const double* __restrict__ pairs, int6
 
 // Workspace partials: pairs (sum, non-finite count) per workgroup at partials[2 blk],
 // partials[2 blk + 1]; the header partials[-2] (= workspace[0]) is the number of
-// pairs.  With out_sum, the LAST workgroup to finish (a ticket counter at
-// partials[-1] = workspace[1], zero before the call and left zero after it) sums every
-// pair in fixed order into out_sum = {sum, non-finite count}: no reduction launch.
+// pairs.  With out_sum, the LAST workgroup to finish sums every pair in fixed order into
+// out_sum = {sum, non-finite count}: no reduction launch.  The last workgroup is found
+// on a 64-bit ticket at partials[-1] = workspace[1], (epoch << 32 | count): the host
+// gives every summed call a non-zero epoch, a workgroup that finds another epoch there
+// (a finished call leaves 0; a fresh workspace holds anything) starts this call's count
+// at 1 (compare-and-swap from what it saw), the others add 1; the workgroup that brings
+// the count to gridDim.x is the last and clears the ticket.  So the workspace needs no
+// initialisation and the call no memset launch (a replayed graph repeats its epoch,
+// which the clear makes safe).
 // Only the pairs cross workgroups, so they are written and read as agent-scope
 // atomics (coherent across the XCDs' separate L2s) and ordered before the ticket by a
 // vmcnt(0) wait: no release / acquire fence, which would write back / invalidate the
 // whole L2 in every workgroup.  The ticket is a vector atomic.  `red` holds
 // 2 * kMaxBlock / 64 doubles.  Contains __syncthreads: call from every thread.
 __device__ __forceinline__ void write_partial(double* partials, double acc, int nf, double* red,
-                                              double* out_sum, int64_t base = 0) {
+                                              double* out_sum, uint32_t epoch, int64_t base = 0) {
   double c = (double)nf;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -854,13 +861,23 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
     if (blockIdx.x == 0) partials[-2] = (double)(base + gridDim.x);  // workspace header: number of pairs
   }
   if (out_sum == nullptr) return;  // partials-only launch (nfn_reduce_partials_f64 finishes it)
-  unsigned* ticket = reinterpret_cast<unsigned*>(partials - 1);
+  unsigned long long* ticket = reinterpret_cast<unsigned long long*>(partials - 1);
   int* flag = reinterpret_cast<int*>(red);
   __syncthreads();  // red is free again
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pair has reached the coherence point
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = prev == gridDim.x - 1;
+    // Only a workgroup that still sees another epoch tries to install this one (a CAS from
+    // the value it saw, so it cannot undo another's install); every other workgroup adds 1.
+    // A CAS per workgroup would serialise the whole grid's finish (+0.7 ms at C2, measured).
+    unsigned long long cur = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned count = 0u;
+    if ((unsigned)(cur >> 32) != epoch &&
+        __hip_atomic_compare_exchange_strong(ticket, &cur, ((unsigned long long)epoch << 32) | 1ull,
+                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      count = 1u;
+    else
+      count = (unsigned)__hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    flag[0] = count == gridDim.x;
   }
   __syncthreads();
   const bool last = flag[0] != 0;
@@ -870,7 +887,7 @@ __device__ __forceinline__ void write_partial(double* partials, double acc, int 
   // stored before their ticket increments, are visible to its loads below.
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   sum_pairs<true>(partials, base + gridDim.x, red, out_sum);
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -899,7 +916,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_logprob_kernel(ChainArgs a) {
     lp = eval_sample<DM, FAST>(z, lds + (tb ? 0 : tid * a.lds_stride), a) - corr;
     if (a.out) a.out[b] = lp;
   }
-  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red, a.out_sum, a.pair_base);
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)lp : 0.0, tid < nr ? nonfinite1(lp) : 0, red, a.out_sum, a.epoch, a.pair_base);
 }
 
 // Posterior: the same tile walk once per draw, with an online logsumexp over draws.
@@ -936,7 +953,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_lse_kernel(ChainArgs a) {
     res = lse_finish<FAST>(m, acc, a.S);
     if (a.out) a.out[b0 + tid] = res;
   }
-  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red, a.out_sum, a.pair_base);
+  if (a.partials) write_partial(a.partials, tid < nr ? (double)res : 0.0, tid < nr ? nonfinite1(res) : 0, red, a.out_sum, a.epoch, a.pair_base);
 }
 
 // Persistent, software-pipelined version of the two kernels above (the hot path).
@@ -1145,7 +1162,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     }
   }
   if (a.partials && (!POST || nsp == 1)) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 
@@ -1302,7 +1319,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   }
   flush();
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 
@@ -1434,7 +1451,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs
     rg = rgn;
   }
   flush();
-  if (a.partials && nsp == 1) write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.pair_base);
+  if (a.partials && nsp == 1) write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
 }
 
 // Combines the per-range (max, scaled sum) pairs of a draw-split posterior:
@@ -1443,7 +1460,7 @@ template <bool FAST>
 __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2* __restrict__ parts, int nsplit,
                                                                      int S, int64_t B, float* __restrict__ out,
                                                                      double* __restrict__ partials,
-                                                                     double* __restrict__ out_sum) {
+                                                                     double* __restrict__ out_sum, uint32_t epoch) {
   __shared__ double red[2 * kMaxBlock / 64];
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float res = 0.0f;
@@ -1469,7 +1486,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_merge_kernel(const float2
     }
     if (out) out[b] = res;
   }
-  if (partials) write_partial(partials, b < B ? (double)res : 0.0, b < B ? nonfinite1(res) : 0, red, out_sum);
+  if (partials) write_partial(partials, b < B ? (double)res : 0.0, b < B ? nonfinite1(res) : 0, red, out_sum, epoch);
 }
 
 // ---------------------------------------------------------------------------
@@ -1799,7 +1816,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
   }
   if (pend_b >= 0 && a.out) a.out[pend_b] = pend_v;
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 
@@ -1910,7 +1927,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   }
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
   if (a.partials) {
-    write_partial(a.partials, acc, nfc, red, a.out_sum, a.pair_base);
+    write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
 }
 

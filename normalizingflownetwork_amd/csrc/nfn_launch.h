@@ -142,6 +142,6 @@ void launch_grid(bool fast, int dm, const GridArgs& ga, dim3 grid, dim3 block, s
 void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);
 void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,
-                            double* out_sum, hipStream_t s);
+                            double* out_sum, uint32_t epoch, hipStream_t s);
 
 }  // namespace nfn

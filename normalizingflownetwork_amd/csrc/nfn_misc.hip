@@ -45,14 +45,14 @@ void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s) 
 }
 
 void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,
-                            double* out_sum, hipStream_t s) {
+                            double* out_sum, uint32_t epoch, hipStream_t s) {
   const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
   if (fast)
     hipLaunchKernelGGL(posterior_merge_kernel<true>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, parts, nsplit, S, B,
-                       out, partials, out_sum);
+                       out, partials, out_sum, epoch);
   else
     hipLaunchKernelGGL(posterior_merge_kernel<false>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, parts, nsplit, S,
-                       B, out, partials, out_sum);
+                       B, out, partials, out_sum, epoch);
 }
 
 }  // namespace nfn

@@ -79,8 +79,8 @@ WORKSPACE_CACHE_ENTRIES = 8
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
     """The workspace of the current (device, stream): calls are ordered on their stream,
     so calls in flight on different streams never share partials, the posterior's split
-    region or the finishing ticket.  No initialisation is needed (ABI 200: every summed
-    call clears its ticket on the stream).  Dropping an entry is safe: its memory returns
+    region or the finishing ticket.  No initialisation is needed (ABI 200: the ticket
+    carries a per-call epoch).  Dropping an entry is safe: its memory returns
     to the caching allocator's pool of the SAME stream, so a later allocation that reuses
     it is ordered after the calls that used it."""
     key = (device.index, int(torch.cuda.current_stream(device).cuda_stream))
@@ -745,10 +745,14 @@ class FlowsLauncher:
     single-flow launches (``nfn_flow_fwd_ldj_f32``, PlanarFlow.py:68-80 / RadialFlow.py:50-70 /
     AffineFlow.py called one bijector at a time), each reading its own block of every row
     of ``t`` (the layer's reversed layout) and the previous flow's z, writing z and its own
-    log|det J| (``ldj`` (K, B)).  ``z_out`` holds z_K after ``launch()``."""
+    log|det J| (``ldj`` (K, B)).  ``z_out`` holds z_K after ``launch()``.
+
+    ``separate=True``: the flows are built individually, each over its own contiguous
+    (B, param_size) parameter tensor (copied from its block of ``t`` here, once), instead of
+    as views of the one wide ``t`` — the case where a launch reads only its own bytes."""
 
     def __init__(self, z: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
-                 trainable_base: bool):
+                 trainable_base: bool, separate: bool = False):
         self.lib = _lib.load()
         dev = z.device
         d = int(n_dims)
@@ -765,11 +769,18 @@ class FlowsLauncher:
         self.ldj = torch.empty((max(1, K), B), dtype=torch.float32, device=dev)
         self.z_out = zs[(K - 1) % 2] if K else z
         self._calls = []
+        self.params = []  # separate=True: the flows' own parameter tensors (kept alive here)
         zin = z
         for k, f in enumerate(flow_types):
             zo = zs[k % 2]
-            self._calls.append((FLOW_IDS[f], _ptr(zin), _row_stride(zin), _ptr(t) + 4 * offs[k], _row_stride(t), B, d,
-                                _ptr(zo), _ptr(self.ldj[k])))
+            if separate:
+                pk = t[:, offs[k]:offs[k] + param_size(f, d)].contiguous()
+                self.params.append(pk)
+                pptr, pstride = _ptr(pk), _row_stride(pk)
+            else:
+                pptr, pstride = _ptr(t) + 4 * offs[k], _row_stride(t)
+            self._calls.append((FLOW_IDS[f], _ptr(zin), _row_stride(zin), pptr, pstride, B, d, _ptr(zo),
+                                _ptr(self.ldj[k])))
             zin = zo
         self.bytes_per_launch = float(B) * sum(4 * d + 4 * param_size(f, d) + 4 * d + 4 for f in flow_types)
 

@@ -289,8 +289,8 @@ def test_chunked_batch(ft, d, B, gpu):
 @pytest.mark.parametrize("kind", ["chain", "chain_chunked", "posterior", "dense"])
 def test_uninitialised_workspace(kind, gpu):
     """ABI 200: a workspace from plain allocation — here filled with garbage,
-    the finishing ticket included — gives the same fp64 sum as a zeroed one: every summed
-    call clears its ticket on the stream before launching."""
+    the finishing ticket included — gives the same fp64 sum as a zeroed one: the ticket
+    carries a per-call epoch that the garbage does not (write_partial, nfn_device.h)."""
     from normalizingflownetwork_amd import _lib
 
     lib = _lib.load()
@@ -339,3 +339,58 @@ def test_uninitialised_workspace(kind, gpu):
     if fin.all():
         assert float(res[0][0][0].item()) == pytest.approx(float(res[0][1].double().sum().item()), rel=1e-12)
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("kind", ["chain", "posterior_split"])
+def test_graph_replay_repeats_epoch(kind, gpu):
+    """A summed call captured in a HIP graph replays with the SAME ticket epoch every time
+    (write_partial, nfn_device.h): the last workgroup's clear of the ticket is what makes
+    the next replay count from one.  Three replays over changing inputs (written into the
+    graph's static t between replays), each sum against its own values, and the first
+    against an eager call."""
+    from normalizingflownetwork_amd import _lib
+
+    lib = _lib.load()
+    ids, k = _ids(C2)
+    p_ids = ctypes.cast(ids, ctypes.c_void_p)
+    B, S = (200_000, 1) if kind == "chain" else (30_000, 8)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    y = torch.randn((B, 1), generator=gen, device="cuda")
+    t = torch.randn((S, B, 32), generator=gen, device="cuda")
+    n = int(lib.nfn_chain_workspace_doubles(B, 1, 32) if kind == "chain" else lib.nfn_posterior_workspace_doubles(B, 1, 32))
+    ws = torch.empty((n,), dtype=torch.float64, device="cuda")
+    ws.view(torch.int32).fill_(0x5A5A5A5A)
+    osum = torch.empty((2,), dtype=torch.float64, device="cuda")
+    out = torch.empty((B,), dtype=torch.float32, device="cuda")
+
+    def call(stream):
+        if kind == "chain":
+            rc = lib.nfn_chain_logprob_f32(y.data_ptr(), 1, t.data_ptr(), 32, B, 1, p_ids, k, 1, None, None,
+                                           out.data_ptr(), osum.data_ptr(), ws.data_ptr(), stream)
+        else:
+            rc = lib.nfn_posterior_lse_f32(y.data_ptr(), 1, t.data_ptr(), B * 32, 32, S, B, 1, p_ids, k, 1, None,
+                                           None, out.data_ptr(), osum.data_ptr(), ws.data_ptr(), stream)
+        _lib.check(rc, kind)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        call(ctypes.c_void_p(side.cuda_stream))  # eager, on the capture stream
+    torch.cuda.synchronize()
+    eager = (osum.clone(), out.clone())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        call(ctypes.c_void_p(side.cuda_stream))
+    torch.cuda.synchronize()
+    for r in range(3):
+        if r:
+            t.copy_(torch.randn((S, B, 32), generator=gen, device="cuda"))
+        osum.fill_(-1.0)
+        g.replay()
+        torch.cuda.synchronize()
+        if r == 0:
+            assert torch.equal(out, eager[1]) and torch.equal(osum, eager[0])
+        assert torch.isfinite(out).all()
+        assert float(osum[0].item()) == pytest.approx(float(out.double().sum().item()), rel=1e-12), r
+        assert float(osum[1].item()) == 0.0
+        assert int(ws[1].item()) == 0, "the ticket is left at zero"
