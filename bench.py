@@ -14,7 +14,7 @@ all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
 resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
-                  [--mode forward|grad|dense|dense_grad|bijector]
+                  [--mode forward|grad|dense|dense_grad|bijector|flows [--flow-params views|separate]]
   N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
   bench.py --gpus N), or plain `python bench.py --gpus N`, which starts that launcher as a
   child process itself (before touching the GPU) and exits with its status.
@@ -278,6 +278,10 @@ def main():
                          "layer's flows in one launch (no base density); flows = the same Chain flow by flow, "
                          "one single-flow launch per flow (nfn_flow_fwd_ldj_f32)")
     ap.add_argument("--hidden", type=int, default=16, help="--mode dense / dense_grad: hidden width H")
+    ap.add_argument("--flow-params", default="views", choices=["views", "separate"],
+                    help="--mode flows: the flows' parameters as views of the layer's one wide t (each "
+                         "launch reads whole 128-B rows), or built individually over their own "
+                         "contiguous (B, param_size) tensors")
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the all-reduce even at N = 1 (tests)")
     ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
@@ -328,7 +332,10 @@ def main():
     elif args.mode in ("bijector", "flows"):
         assert S is None, "--mode bijector / flows cover the plain chain configs (C2, C3)"
         t = torch.randn((B, P), generator=gen, device=dev)
-        launcher = (ops.BijectorLauncher if args.mode == "bijector" else ops.FlowsLauncher)(y, t, ft, d, True)
+        if args.mode == "bijector":
+            launcher = ops.BijectorLauncher(y, t, ft, d, True)
+        else:
+            launcher = ops.FlowsLauncher(y, t, ft, d, True, separate=args.flow_params == "separate")
     else:
         t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
         if grad_mode:
@@ -537,7 +544,9 @@ def main():
             bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense", "dense_grad": "_dense_grad",
-                                                           "bijector": "_bijector", "flows": "_flows"}.get(args.mode, ""), B)
+                                                           "bijector": "_bijector",
+                                                           "flows": "_flows" if args.flow_params == "views" else "_flows_separate"
+                                                           }.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline("bijector" if args.mode == "flows" else args.mode, args.config, H=H,
@@ -602,6 +611,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "allreduce": None if (world == 1 or grad_mode) else args.allreduce,
                 "mode": args.mode,
+                **({"flow_params": args.flow_params} if args.mode == "flows" else {}),
             },
             "roofline": {
                 "bound": "hbm",

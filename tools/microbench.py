@@ -528,6 +528,11 @@ def main():
             run(cfg, [{"name": "default", "env": {}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
                       {"name": "wg4", "env": {"NFN_WG_PER_CU": 4}}], rounds=4)
         return
+    if which[0] == "gradab":  # the fused backward: full vs memory-only (flows skipped) vs compute-only (one tile)
+        for cfg in ("C2", "C3"):
+            run_grad(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                           {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}], rounds=4)
+        return
     if which[0] == "gradshape":  # the fused backward: persistent wave tiles vs one tile per workgroup
         for cfg in ("C2",):
             run_grad(cfg, [{"name": "wave_persistent", "env": {}},
