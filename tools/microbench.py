@@ -528,6 +528,44 @@ def main():
             run(cfg, [{"name": "default", "env": {}}, {"name": "wg3", "env": {"NFN_WG_PER_CU": 3}},
                       {"name": "wg4", "env": {"NFN_WG_PER_CU": 4}}], rounds=4)
         return
+    if which[0] == "evcost":  # what per-launch timing events cost the step loop (C2, C5)
+        for cfg in ("C2", "C5"):
+            ft, d, B, S = CFG[cfg]
+            P = ops.total_param_size(ft, d, True)
+            gen = torch.Generator(device="cuda").manual_seed(1)
+            y = torch.randn((B, d), generator=gen, device="cuda")
+            t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device="cuda")
+            L = ops.ChainLauncher(y, t, ft, d, True, draws=S)
+            stream = torch.cuda.current_stream()
+            sh = int(stream.cuda_stream)
+            prewarm(lambda: L.launch(sh))
+            K = 200
+            res = {"none": [], "per_launch": [], "region": []}
+            for r in range(4):
+                for mode in res:
+                    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    if mode == "region":
+                        evs[0][0].record(stream)
+                    for e0, e1 in evs:
+                        if mode == "per_launch":
+                            e0.record(stream)
+                        L.launch(sh)
+                        if mode == "per_launch":
+                            e1.record(stream)
+                    if mode == "region":
+                        evs[0][1].record(stream)
+                    torch.cuda.synchronize()
+                    wall = (time.perf_counter() - t0) * 1e3 / K
+                    kern = (float(np.mean([a.elapsed_time(b) for a, b in evs])) if mode == "per_launch"
+                            else evs[0][0].elapsed_time(evs[0][1]) / K if mode == "region" else None)
+                    res[mode].append((wall, kern))
+            for mode, v in res.items():
+                print(json.dumps({"cfg": cfg, "events": mode, "wall_ms_per_launch": float(np.median([w for w, _ in v])),
+                                  "event_ms_per_launch": (float(np.median([k for _, k in v])) if v[0][1] is not None else None),
+                                  "rounds": v}), flush=True)
+        return
     if which[0] == "gradab":  # the fused backward: full vs memory-only (flows skipped) vs compute-only (one tile)
         for cfg in ("C2", "C3"):
             run_grad(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
