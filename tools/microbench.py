@@ -566,6 +566,11 @@ def main():
                                   "event_ms_per_launch": (float(np.median([k for _, k in v])) if v[0][1] is not None else None),
                                   "rounds": v}), flush=True)
         return
+    if which[0] == "fwdab":  # forward kernels: full vs memory-only (flows skipped) vs compute-only (one tile)
+        for cfg in ("C5", "C2", "C3"):
+            run(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                      {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}], rounds=4)
+        return
     if which[0] == "gradab":  # the fused backward: full vs memory-only (flows skipped) vs compute-only (one tile)
         for cfg in ("C2", "C3"):
             run_grad(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
