@@ -647,6 +647,52 @@ __device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, u
   return l2;
 }
 
+// chain1_fast_pairs over TWO rows that share the program (two draws of one sample in the
+// posterior): one dispatch per pair of flows for both, two independent dependency chains
+// for the scheduler to interleave.  Per row the same arithmetic as chain1_fast_pairs.
+template <int ST = 1>
+__device__ __forceinline__ void chain1_fast_pairs2(float& za, float& zb, const float* rowa, const float* rowb,
+                                                   uint32_t types, int K, int P, float& l2a, float& l2b) {
+  l2a = 0.0f;
+  l2b = 0.0f;
+  int ia = type1(types, 0), ib = type1(types, 1);
+  int offa = max(P - size1(ia), 0), offb = max(offa - size1(ib), 0);
+  float pa[3], pb[3], qa[3], qb[3];
+  read3c<ST>(pa, rowa, offa);
+  read3c<ST>(pb, rowa, offb);
+  read3c<ST>(qa, rowb, offa);
+  read3c<ST>(qb, rowb, offb);
+#pragma unroll 1
+  for (int k = 0; k + 1 < K; k += 2) {
+    const int ian = type1(types, k + 2), ibn = type1(types, k + 3);
+    const int offan = max(offb - size1(ian), 0), offbn = max(offan - size1(ibn), 0);
+    float pna[3], pnb[3], qna[3], qnb[3];
+    read3c<ST>(pna, rowa, offan);
+    read3c<ST>(pnb, rowa, offbn);
+    read3c<ST>(qna, rowb, offan);
+    read3c<ST>(qnb, rowb, offbn);
+#define NFN_FWD2(A, B)                   \
+  flow_pair1<A, B>(za, l2a, pa, pb);     \
+  flow_pair1<A, B>(zb, l2b, qa, qb)
+    NFN_PAIR_SWITCH(ia * 3 + ib, NFN_FWD2)
+#undef NFN_FWD2
+    ia = ian;
+    ib = ibn;
+    offb = offbn;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pa[i] = pna[i];
+      pb[i] = pnb[i];
+      qa[i] = qna[i];
+      qb[i] = qnb[i];
+    }
+  }
+  if (K & 1) {
+    l2a += __builtin_amdgcn_logf(fabsf(flow1_fast(ia, za, pa)));
+    l2b += __builtin_amdgcn_logf(fabsf(flow1_fast(ia, zb, qa)));
+  }
+}
+
 // Chain-evaluation form of the d = 1 kernels: the packed loop, two flows per dispatch,
 // or (diagnostic experiment) one compile-time program, C2's.
 constexpr int kChainLoop = 0, kStaticProg = 2, kChainPairs = 3;
@@ -1452,6 +1498,127 @@ __global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs
   }
   flush();
   if (a.partials && nsp == 1) write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
+}
+
+// posterior_wave1_kernel with TWO draws per step (diagnostic experiment, nsplit == 1):
+// each lane evaluates its sample under draws s and s + 1 (chain1_fast_pairs2), the rows
+// of both draws go to two LDS slots behind one counted wait, and the next step's two
+// draws are in flight meanwhile (16 KiB per wave).  The logsumexp takes the draws in the
+// same order, so the score is bitwise posterior_wave1_kernel<Q, true, kChainPairs>'s.
+template <int Q>
+__global__ void __launch_bounds__(kMaxBlock, 2) posterior_wave1x2_kernel(ChainArgs a) {
+  extern __shared__ float lds[];
+  __shared__ double red[2 * kMaxBlock / 64];
+  constexpr int RSTEP = 64 / Q;
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int LS = a.lds_stride;
+  const int64_t rs = a.t_rowstride, ds = a.t_drawstride;
+  const int r0 = lane / Q, c4 = lane % Q;
+  float* tl0 = lds + wid * 2 * 64 * LS;
+  float* tl1 = tl0 + 64 * LS;
+  const int l0 = r0 * LS + 4 * c4;
+  const int S = a.S;
+  const int64_t ntiles = a.ntiles;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int toff = (r0 * (int)rs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)rs * 4;
+  const float logS = f_log<true>((float)S);
+  const bool trainable = a.trainable != 0;
+  const uint32_t types = a.prog.types[0];
+  const int K = a.prog.K;
+
+  float4 buf0[Q], buf1[Q];
+  float ybuf;
+  // rows of draws s and s + 1 of tile `tl_` (an empty descriptor past S or past the end)
+  auto issue = [&](int64_t tl_, int s) {
+    const int64_t b0 = tl_ * 64;
+    const int64_t nr = tl_ < ntiles ? min((int64_t)64, a.B - b0) : 0;
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const int64_t span = nr > 0 ? ((nr - 1) * rs + a.P) * 4 : 0;
+    const auto rt0 = tile_rsrc(a.t + (nr > 0 ? s * ds + b0c * rs : 0), span);
+    const bool has1 = s + 1 < S;
+    const auto rt1 = tile_rsrc(a.t + (nr > 0 && has1 ? (s + 1) * ds + b0c * rs : 0), has1 ? span : 0);
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+      buf0[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt0, toff, k * kstep, kNT));
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+      buf1[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt1, toff, k * kstep, kNT));
+  };
+
+  double acc_sum = 0.0;
+  int nfc = 0;
+  const __amdgpu_buffer_rsrc_t empty_r = tile_rsrc(a.out, 0);
+  __amdgpu_buffer_rsrc_t pend_r = empty_r;
+  float pend_v = 0.0f;
+  auto flush = [&]() {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  };
+  issue(tile, 0);
+  flush();
+  while (tile < ntiles) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = min((int64_t)64, a.B - b0);
+    const int64_t tilen = tile + ustep;
+    float m = -INFINITY, lacc = 0.0f, z0 = 0.0f;
+    for (int s = 0; s < S; s += 2) {
+      if (a.prio) __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        float* d0 = tl0 + l0 + k * RSTEP * LS;
+        d0[0] = buf0[k].x;
+        d0[1] = buf0[k].y;
+        d0[2] = buf0[k].z;
+        d0[3] = buf0[k].w;
+        float* d1 = tl1 + l0 + k * RSTEP * LS;
+        d1[0] = buf1[k].x;
+        d1[1] = buf1[k].y;
+        d1[2] = buf1[k].z;
+        d1[3] = buf1[k].w;
+      }
+      if (s == 0) z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+      wave_lds_sync();
+      if (s + 2 < S)
+        issue(tile, s + 2);
+      else
+        issue(tilen, 0);
+      flush();
+      pend_r = empty_r;
+      if (a.prio) __builtin_amdgcn_s_setprio(0);
+      float za = z0, zb = z0, l2a = 0.0f, l2b = 0.0f;
+      if (K > 0) chain1_fast_pairs2<1>(za, zb, tl0 + lane * LS, tl1 + lane * LS, types, K, a.P, l2a, l2b);
+      const float lpa = (base1_fast<1>(za, tl0 + lane * LS, trainable) + l2a * kLn2) - corr;
+      lse_push<true>(m, lacc, lpa);
+      if (s + 1 < S) {
+        const float lpb = (base1_fast<1>(zb, tl1 + lane * LS, trainable) + l2b * kLn2) - corr;
+        lse_push<true>(m, lacc, lpb);
+      }
+      wave_lds_sync();
+    }
+    const float res = ((m == -INFINITY || m != m) ? m : m + f_log<true>(lacc)) - logS;
+    if (lane < nr) {
+      acc_sum += (double)res;
+      nfc += nonfinite1(res);
+    }
+    pend_v = res;
+    pend_r = tile_rsrc(a.out ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+    tile = tilen;
+  }
+  flush();
+  if (a.partials) write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
 }
 
 // Combines the per-range (max, scaled sum) pairs of a draw-split posterior:

@@ -130,6 +130,13 @@ void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out
   const int64_t units = a.ntiles * a.nsplit;
   const int64_t grid = cap_grid(std::min<int64_t>((units + 3) / 4, (int64_t)cu_count() * posterior_wave1_wgs_per_cu()), a);
   *grid_out = grid;
+#ifdef NFN_DIAG
+  // experiment: two draws per step (posterior_wave1x2_kernel), whole-tile units only
+  if (env_int("NFN_POST_X2", 0) == 1 && a.nsplit == 1 && a.prog.K <= 16) {
+    hipLaunchKernelGGL(posterior_wave1x2_kernel<Q>, dim3((unsigned)grid), dim3(kMaxBlock), 2 * (lds - 16) + 16, s, a);
+    return;
+  }
+#endif
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
 }
 #endif

@@ -566,6 +566,11 @@ def main():
                                   "event_ms_per_launch": (float(np.median([k for _, k in v])) if v[0][1] is not None else None),
                                   "rounds": v}), flush=True)
         return
+    if which[0] == "postx2":  # C5 posterior: two draws per step (NFN_POST_X2) vs one
+        run("C5", [{"name": "one_draw", "env": {}}, {"name": "two_draws", "env": {"NFN_POST_X2": 1}},
+                   {"name": "two_draws_wg1", "env": {"NFN_POST_X2": 1, "NFN_WG_PER_CU": 1}},
+                   {"name": "one_draw_b", "env": {}}], rounds=4)
+        return
     if which[0] == "fwdab":  # forward kernels: full vs memory-only (flows skipped) vs compute-only (one tile)
         for cfg in ("C5", "C2", "C3"):
             run(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
