@@ -138,7 +138,9 @@ int64_t nfn_chain_workspace_doubles(int64_t B, int32_t d, int32_t P);
  *   workspace  : device double[nfn_chain_workspace_doubles(B, d, P)] when out_sum != NULL.
  *                Needs no initialisation (e.g. a plain hipMalloc): the finishing ticket
  *                (workspace[1]) is tagged with a per-call epoch, so a stale or garbage
- *                ticket restarts the count (no memset launch precedes the kernel).
+ *                ticket restarts the count (no memset launch precedes the kernel; only
+ *                garbage whose upper 32 bits equal the call's epoch, 2^-32 for random
+ *                bits, would be taken for this call's count).
  *                Layout: workspace[0] = number n of per-workgroup pairs written,
  *                workspace[1] = the finishing ticket, workspace[2 + 2i] /
  *                workspace[3 + 2i] = workgroup i's fp64 partial sum / non-finite count.
