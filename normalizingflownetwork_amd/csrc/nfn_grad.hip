@@ -182,6 +182,154 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
   }
 }
 
+#ifdef NFN_DIAG
+// DIAGNOSTIC A/B (NFN_DIAG build, NFN_GRAD_WAVE1=1; measured and not adopted, DESIGN.md
+// "C2 backward: the straight-line pipeline"): bitwise the release kernel's results.
+// d = 1, fast math, P = 4Q (Q in {2, 4, 8, 16}): chain_grad_wave_kernel's walk with
+// chain_wave1_kernel's memory pipeline (C1, C2 backward).  Every tile access is a
+// buffer instruction through a wave-uniform descriptor bounded at B, so the loop body
+// is straight-line code: each iteration issues the same loads (y, g, Q row pieces) and
+// the same stores (log_prob, d/dy, Q gradient pieces; absent outputs go through empty
+// descriptors), the next hand-off waits with vmcnt(#stores) for its prefetched rows and
+// never for the previous tile's gradient stores.  (The generic wave kernel's per-slot
+// branches made the waitcnt pass drain every store before the hand-off.)
+// SPLIT = 2: the next tile's rows are issued in two halves, the second between the
+// chain's forward and reverse passes (half the bytes in flight per wave).
+template <int Q, int CM, int SPLIT = 1>
+__global__ void __launch_bounds__(kMaxBlock) chain_grad_wave1_kernel(GradArgs ga) {
+  const ChainArgs& a = ga.c;
+  extern __shared__ float lds[];
+  constexpr int RSTEP = 64 / Q;  // rows per wave instruction
+  constexpr int kNT = 2;         // non-temporal: streamed once
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.lds_stride;
+  const int K = a.prog.K;
+  const int P = a.P;
+  const int64_t rs = a.t_rowstride;
+  const int64_t gts = ga.gt_rowstride;
+  const int r0 = lane / Q, c4 = lane % Q;
+  float* tl = lds + wid * (64 * S + K * 64);
+  float* zh = tl + 64 * S + lane;
+  const int l0 = r0 * S + 4 * c4;
+  const int64_t ntiles = a.ntiles;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const bool has_g = ga.g_out != nullptr;
+  const bool want_lp = a.out != nullptr;
+  const uint32_t types = a.prog.types[0];
+  const int64_t abl_tile = a.ablate_loads ? u0 : -1;  // diagnostic: compute-only timing
+  // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int toff = (r0 * (int)rs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)rs * 4;
+  const int goff = (r0 * (int)gts + 4 * c4) * 4;
+  const int gkstep = RSTEP * (int)gts * 4;
+
+  constexpr int QA = SPLIT == 2 && Q >= 2 ? Q / 2 : Q;  // row pieces issued with y and g
+  float4 buf[Q];
+  float ybuf, gbuf;
+  auto rows_rsrc = [&](int64_t tile) {
+    if (abl_tile >= 0) tile = abl_tile;
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    return tile_rsrc(a.t + (nr > 0 ? b0 : 0) * rs, nr > 0 ? ((nr - 1) * rs + P) * 4 : 0);
+  };
+  auto issue = [&](int64_t tile) {
+    if (abl_tile >= 0) tile = abl_tile;
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    const auto rg = tile_rsrc(has_g ? ga.g_out + b0c : ga.g_out, has_g ? nr * 4 : 0);
+    const auto rt = rows_rsrc(tile);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    gbuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lane * 4, 0, 0));
+#pragma unroll
+    for (int k = 0; k < QA; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+  };
+  auto issue_rest = [&](int64_t tile) {
+    const auto rt = rows_rsrc(tile);
+#pragma unroll
+    for (int k = QA; k < Q; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+  };
+
+  // A tile's stores: log_prob, d/dy and the gradient rows (read back from the LDS
+  // tile), through descriptors bounded at B — empty ones for absent outputs and for
+  // nr = 0, so every path issues the same stores.
+  auto flush = [&](int64_t b0, int64_t nr, float lp, float gy) {
+    const int64_t no = want_lp ? nr : 0, ny = ga.grad_y ? nr : 0, nt = ga.grad_t ? nr : 0;
+    const auto ro = tile_rsrc(no > 0 ? a.out + b0 : a.out, no * 4);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, lp), ro, lane * 4, 0, kNT);
+    const auto rgy = tile_rsrc(ny > 0 ? ga.grad_y + b0 : ga.grad_y, ny * 4);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gy), rgy, lane * 4, 0, kNT);
+    const auto rgt = tile_rsrc(nt > 0 ? ga.grad_t + b0 * gts : ga.grad_t, nt > 0 ? ((nt - 1) * gts + P) * 4 : 0);
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      const float* src = tl + l0 + k * RSTEP * S;
+      __builtin_amdgcn_raw_buffer_store_b128(f32x4{src[0], src[1], src[2], src[3]}, rgt, goff, k * gkstep, kNT);
+    }
+  };
+
+  issue(u0);
+  issue_rest(u0);
+  flush(0, 0, 0.0f, 0.0f);  // empty: every path into the loop ends [loads][stores] (counted waits)
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = min((int64_t)64, a.B - b0);
+    if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      float* dst = tl + l0 + k * RSTEP * S;
+      dst[0] = buf[k].x;
+      dst[1] = buf[k].y;
+      dst[2] = buf[k].z;
+      dst[3] = buf[k].w;
+    }
+    float z = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+    const float gl = has_g ? gbuf : 1.0f;
+    wave_lds_sync();
+    issue(tile + ustep);
+    if (a.prio) __builtin_amdgcn_s_setprio(0);
+    const int64_t next = tile + ustep;
+    auto mid = [&]() {
+      if constexpr (QA < Q) issue_rest(next);
+    };
+    float adj;
+    // rows past B (the last tile) run on zeros; their stores fall outside the descriptors
+    const float lp = (CM == kChainPairs ? grad1_pairs(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl,
+                                                      want_lp, adj, mid)
+                                        : grad1_packed(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl,
+                                                       want_lp, adj, mid)) -
+                     corr;
+    wave_lds_sync();
+    flush(b0, nr, lp, norm ? f_div<true>(adj, ystd) : adj);
+    wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
+  }
+}
+
+template <int Q>
+bool launch_wave1_q(const GradArgs& ga, size_t lds_block, int wpb, hipStream_t s, int64_t* grid) {
+  const int cm = env_int("NFN_CHAIN_FORM", ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop);
+  auto k = cm == kChainPairs ? chain_grad_wave1_kernel<Q, kChainPairs> : chain_grad_wave1_kernel<Q, kChainLoop>;
+  if (env_int("NFN_GRAD_SPLIT", 1) == 2)
+    k = cm == kChainPairs ? chain_grad_wave1_kernel<Q, kChainPairs, 2> : chain_grad_wave1_kernel<Q, kChainLoop, 2>;
+  const int T = 64 * wpb;
+  *grid = std::max<int64_t>(1, persistent_grid(k, T, lds_block, (ga.c.ntiles + wpb - 1) / wpb));
+  k<<<dim3((unsigned)*grid), dim3(T), lds_block, s>>>(ga);
+  return true;
+}
+#endif  // NFN_DIAG
+
 template <bool FAST>
 void launch_grad_t(int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_t s) {
   switch (dm) {
@@ -243,6 +391,21 @@ void launch_grad(bool fast, int dm, const GradArgs& ga, dim3 grid, size_t lds, h
 
 bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_block, int waves_per_block,
                       hipStream_t s, int64_t* grid) {
+#ifdef NFN_DIAG
+  // diagnostic A/B: d = 1 fast math with 64-row tiles spanning < 2 GiB on the straight-line
+  // buffer pipeline (NFN_GRAD_WAVE1=1)
+  const ChainArgs& a = ga.c;
+  if (fast && dm == 1 && a.d == 1 && a.prog.K <= 16 && a.t_rowstride * 64 * 4 < ((int64_t)1 << 31) &&
+      ga.gt_rowstride * 64 * 4 < ((int64_t)1 << 31) && a.y_bstride * 64 * 4 < ((int64_t)1 << 31) &&
+      env_int("NFN_GRAD_WAVE1", 0) == 1) {
+    switch (nv) {
+      case 2: return launch_wave1_q<2>(ga, lds_block, waves_per_block, s, grid);
+      case 4: return launch_wave1_q<4>(ga, lds_block, waves_per_block, s, grid);
+      case 8: return launch_wave1_q<8>(ga, lds_block, waves_per_block, s, grid);
+      case 16: return launch_wave1_q<16>(ga, lds_block, waves_per_block, s, grid);
+    }
+  }
+#endif
   return fast ? launch_wave_t<true>(dm, nv, ga, lds_block, waves_per_block, s, grid)
               : launch_wave_t<false>(dm, nv, ga, lds_block, waves_per_block, s, grid);
 }

@@ -301,9 +301,16 @@ __device__ __forceinline__ void flow1_bwd(int id, float z, float& a, const float
 // passes read the NEXT flow's parameters (and, in reverse, its input z) from LDS
 // before evaluating the current flow.  ST: floats between a sample's consecutive
 // parameters (see planar1_bwd).
-template <int ST = 1>
+// Called once between the forward and the reverse pass of grad1_packed / grad1_pairs
+// (the streaming backward may issue part of its next-tile prefetch there).
+struct NoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+template <int ST = 1, class Mid = NoMid>
 __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, int zs, uint32_t types, int K, int P,
-                                              bool trainable, float gl, bool want_lp, float& adj) {
+                                              bool trainable, float gl, bool want_lp, float& adj,
+                                              const Mid& mid = Mid{}) {
   float l2 = 0.0f;
   int id = (int)(types & 3u);
   int off = max(P - size1(id), 0);
@@ -334,6 +341,7 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
     }
   }
   const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  mid();
   float a1;
   if (trainable) {
     float sps, sgs;
@@ -412,9 +420,10 @@ __device__ __forceinline__ void bwd_pair1(float& a1, float* row, float za, float
   flow1_bwd<ST>(IB, zb, a1, pb, row + obb * ST, gl);
 }
 
-template <int ST = 1>
+template <int ST = 1, class Mid = NoMid>
 __device__ __forceinline__ float grad1_pairs(float& z, float* row, float* zh, int zs, uint32_t types, int K, int P,
-                                             bool trainable, float gl, bool want_lp, float& adj) {
+                                             bool trainable, float gl, bool want_lp, float& adj,
+                                             const Mid& mid = Mid{}) {
   float l2 = 0.0f;
   int ia = type1(types, 0), ib = type1(types, 1);
   int offa = max(P - size1(ia), 0), offb = max(offa - size1(ib), 0);
@@ -454,6 +463,7 @@ __device__ __forceinline__ float grad1_pairs(float& z, float* row, float* zh, in
       flow1_z(ia, z, pa);
   }
   const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  mid();
   float a1;
   if (trainable) {
     float sps, sgs;

@@ -3,6 +3,8 @@
   python tests/diag_modes.py strategies   -- NFN_DIAG build: every tile-streaming strategy
       (NFN_LOAD_MODE) gives bitwise-identical per-sample log_prob, and the draw-split
       posterior agrees with the single-range one (NFN_POST_SPLIT=1)
+  python tests/diag_modes.py grad_stream  -- NFN_DIAG build: the d = 1 straight-line
+      backward (NFN_GRAD_WAVE1=1) equals the release's generic wave kernel bitwise
   python tests/diag_modes.py release      -- release build under ablation / tuning knobs in
       the environment: results are the oracle's (the knobs are compiled out)
 Prints one JSON line; exits non-zero on a mismatch."""
@@ -63,6 +65,44 @@ def strategies():
     return res
 
 
+def grad_stream():
+    """d = 1 backward: the straight-line buffer pipeline (chain_grad_wave1_kernel, diag
+    NFN_GRAD_WAVE1=1, in one or two prefetch pieces) against the release's generic wave
+    kernel: the same per-sample math, so log_prob, d/dt and d/dy must be bitwise equal
+    (NaN where both are)."""
+    import torch
+
+    from normalizingflownetwork_amd import _lib
+
+    _lib.use_diagnostic_build()
+    from normalizingflownetwork_amd import ops
+
+    res = {"library": os.path.basename(_lib.LIB_PATH)}
+    cases = [(("planar", "radial") * 5, 1 << 20, None), (("planar", "radial") * 5, 4099, (0.3, 1.6)),
+             (("radial", "radial"), 777, None), (("planar", "radial", "planar", "radial", "affine"), 5000, None)]
+    for ft, B, norm in cases:
+        P = ops.total_param_size(ft, 1, True)
+        gen = torch.Generator(device="cuda").manual_seed(B)
+        y = torch.randn((B, 1), generator=gen, device="cuda")
+        t = torch.randn((B, P), generator=gen, device="cuda")
+        g = torch.randn((B,), generator=gen, device="cuda")
+        ym, ys = (np.float32([norm[0]]), np.float32([norm[1]])) if norm else (None, None)
+        outs = {}
+        for v, split in (("0", "1"), ("1", "1"), ("1", "2")):
+            os.environ["NFN_GRAD_WAVE1"], os.environ["NFN_GRAD_SPLIT"] = v, split
+            try:
+                outs[v + split] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
+            finally:
+                os.environ.pop("NFN_GRAD_WAVE1")
+                os.environ.pop("NFN_GRAD_SPLIT")
+        for alt in ("11", "12"):
+            for a, b, what in zip(outs[alt], outs["01"], ("log_prob", "grad_t", "grad_y")):
+                same = (a == b) | (torch.isnan(a) & torch.isnan(b))
+                assert bool(same.all()), f"{ft} B={B} {alt} {what}: {int((~same).sum())} values differ"
+        res[f"P{P}_B{B}"] = "bitwise"
+    return res
+
+
 def release():
     from normalizingflownetwork_amd import _lib, ops
 
@@ -86,4 +126,4 @@ def release():
 
 if __name__ == "__main__":
     which = sys.argv[1]
-    print(json.dumps({which: {"strategies": strategies, "release": release}[which]()}), flush=True)
+    print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream}[which]()}), flush=True)

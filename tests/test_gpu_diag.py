@@ -45,3 +45,9 @@ def test_diag_strategies_bitwise_equal(gpu):
     res = _run("strategies")
     assert res["library"] == "libnfn_hip_diag.so"
     assert all(res[m] == "bitwise" for m in ("coop", "wave", "ownrow", "tile"))
+
+
+def test_diag_grad_stream_bitwise_equal(gpu):
+    res = _run("grad_stream")
+    assert res["library"] == "libnfn_hip_diag.so"
+    assert sum(v == "bitwise" for v in res.values()) == 4

@@ -183,3 +183,61 @@ def test_grad_c3_full_size_sampled_and_broadcast(gpu):
     _, gtb, gyb = _run(gpu, y1, tb, ft, d, True)
     _check(gtb, gt64, dt32, "C3 y-broadcast d/dt")
     _check(gyb, gy64, dy32, "C3 y-broadcast d/dy")
+
+
+@pytest.mark.parametrize("ft", [("planar", "radial"), ("planar", "radial", "planar", "radial", "affine"),
+                                ("planar", "radial") * 5])
+def test_grad_d1_stream_shapes(gpu, ft):
+    """The d = 1 streaming backward (chain_grad_wave_kernel: P = 8, 16, 32) through the
+    C ABI: ragged batches (1, 63, 65, 777 and a multi-wave 9,029 rows), t read from a
+    column slice of a wider buffer, y from a strided column, the gradient rows written
+    into a wider buffer (row stride > P, the pad columns untouched), with and without
+    log_prob / d/dy / an upstream gradient / y normalisation (log_prob is checked on the
+    unnormalised cases, where the forward oracle applies as is)."""
+    import ctypes
+
+    from normalizingflownetwork_amd import _lib, ops
+    from oracle import nfn_oracle as O
+
+    d = 1
+    P = O.total_param_size(ft, d, True)
+    lib = _lib.load()
+    ids, k = ops.flow_ids(ft)
+    rng = np.random.default_rng(11)
+    for case, B in enumerate((1, 63, 65, 777, 9029)):
+        norm, with_g, want_lp, want_gy = case % 2 == 1, case % 3 != 0, case in (0, 2, 4), case != 3
+        y_np = rng.standard_normal((B, d)).astype(np.float32) * 1.5 + 0.3
+        t_np = rng.standard_normal((B, P)).astype(np.float32)
+        g_np = rng.standard_normal(B).astype(np.float32) if with_g else None
+        ym, ys = (np.float32([0.4]), np.float32([1.7])) if norm else (None, None)
+        ywide = torch.zeros((B, 3), device=gpu)
+        ywide[:, 1] = torch.from_numpy(y_np[:, 0]).to(gpu)
+        twide = torch.zeros((B, P + 7), device=gpu)
+        twide[:, :P] = torch.from_numpy(t_np).to(gpu)
+        gts = P + 12
+        gt_buf = torch.full((B, gts), 7.0, device=gpu)
+        gy = torch.empty((B, d), device=gpu) if want_gy else None
+        lp = torch.empty((B,), device=gpu) if want_lp else None
+        gdev = torch.from_numpy(g_np).to(gpu) if with_g else None
+        ymd = torch.from_numpy(ym).to(gpu) if norm else None
+        ysd = torch.from_numpy(ys).to(gpu) if norm else None
+        yv = ywide[:, 1:2]
+        rc = lib.nfn_chain_logprob_grad_f32(
+            yv.data_ptr(), 3, twide.data_ptr(), P + 7, B, d, ctypes.cast(ids, ctypes.c_void_p), k, 1,
+            None if ymd is None else ymd.data_ptr(), None if ysd is None else ysd.data_ptr(),
+            None if gdev is None else gdev.data_ptr(), None if lp is None else lp.data_ptr(), gt_buf.data_ptr(),
+            gts, None if gy is None else gy.data_ptr(), ops._stream())
+        assert rc == 0, _lib.last_error()
+        torch.cuda.synchronize()
+        gt_host = gt_buf.cpu().numpy()
+        assert (gt_host[:, P:] == 7.0).all(), "pad columns of the gradient buffer were written"
+        gt64, dt32, gy64, dy32 = _grads_ref(y_np, t_np, ft, d, True, ym, ys, g_np)
+        tag = f"d1 stream P={P} B={B}"
+        _check(gt_host[:, :P], gt64, dt32, tag + " d/dt")
+        if want_gy:
+            _check(gy.cpu().numpy(), gy64, dy32, tag + " d/dy")
+        if want_lp and not norm:
+            ref64 = O.chain_log_prob(y_np, t_np, ft, d, True, np.float64)
+            ref32 = O.chain_log_prob(y_np, t_np, ft, d, True, np.float32)
+            check_forward(lp.cpu().numpy(), ref64, ref32, tag + " log_prob", nonfinite="match",
+                          sensitivity=fp32_sensitivity(y_np, t_np, ft, d, True))

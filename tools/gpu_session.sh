@@ -173,6 +173,11 @@ for s in $STEPS; do
     gradc3tape) run gradc3tape 300 python tools/microbench.py gradc3tape ;;
     gradc3b128) run gradc3b128 300 python tools/microbench.py gradc3b128 ;;
     c3mem) run c3mem 300 python tools/microbench.py c3mem ;;
+    gradsplit) run gradsplit 400 python tools/microbench.py gradsplit ;;
+    gradw1mem) run gradw1mem 400 python tools/microbench.py gradw1mem ;;
+    gradw1occ) run gradw1occ 400 python tools/microbench.py gradw1occ ;;
+    gradw1) run gradw1 400 python tools/microbench.py gradw1 ;;
+    gradd1tests) run gradd1tests 300 python -u -m pytest tests/test_gpu_grad.py tests/test_gpu_diag.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -581,6 +581,56 @@ def main():
             run_grad(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                            {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}], rounds=4)
         return
+    if which[0] == "gradw1":  # d = 1 backward: straight-line buffer pipeline vs the generic wave kernel
+        for cfg in ("C2", "C1"):
+            G = {"NFN_GRAD_WAVE1": 0}
+            run_grad(cfg, [{"name": "wave1", "env": {"NFN_GRAD_WAVE1": 1}}, {"name": "generic", "env": dict(G)},
+                           {"name": "wave1_memory_only", "env": {"NFN_GRAD_WAVE1": 1, "NFN_ABLATE_FLOWS": 1}},
+                           {"name": "generic_memory_only", "env": dict(G, NFN_ABLATE_FLOWS=1)},
+                           {"name": "wave1_compute_only", "env": {"NFN_GRAD_WAVE1": 1, "NFN_ABLATE_LOADS": 1}},
+                           {"name": "wave1_wpb1", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": 1}},
+                           {"name": "wave1_wpb4", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": 4}},
+                           {"name": "wave1_wg3", "env": {"NFN_GRAD_WAVE1": 1, "NFN_WG_PER_CU": 3}},
+                           {"name": "wave1_wg4", "env": {"NFN_GRAD_WAVE1": 1, "NFN_WG_PER_CU": 4}},
+                           {"name": "wave1_noprio", "env": {"NFN_GRAD_WAVE1": 1, "NFN_PRIO": 0}},
+                           {"name": "wave1_b", "env": {"NFN_GRAD_WAVE1": 1}}, {"name": "generic_b", "env": dict(G)}], rounds=4)
+        return
+    if which[0] == "gradsplit":  # d = 1 backward: next-tile rows in one piece vs two (second half mid-chain)
+        G = {"NFN_GRAD_WAVE1": 0}
+        v = [{"name": "generic", "env": dict(G)}]
+        for wpb, wg in ((2, 0), (4, 3), (1, 12), (2, 4), (4, 2), (1, 8)):
+            e = {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": wpb, "NFN_WG_PER_CU": wg} if wg else {"NFN_GRAD_WAVE1": 1}
+            v.append({"name": f"split1_wpb{wpb}_wg{wg}", "env": dict(e)})
+            v.append({"name": f"split2_wpb{wpb}_wg{wg}", "env": dict(e, NFN_GRAD_SPLIT=2)})
+        v += [{"name": "generic_b", "env": dict(G)}]
+        for cfg in ("C2", "C1"):
+            run_grad(cfg, v, rounds=4)
+        return
+    if which[0] == "gradw1mem":  # d = 1 backward: memory-only stream vs resident waves; full at the best shapes
+        G = {"NFN_GRAD_WAVE1": 0}
+        A = {"NFN_ABLATE_FLOWS": 1}
+        v = [{"name": "generic", "env": dict(G)}, {"name": "wave1_wpb4_wg3", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": 4, "NFN_WG_PER_CU": 3}},
+             {"name": "wave1_wpb1_wg12", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": 1, "NFN_WG_PER_CU": 12}},
+             {"name": "wave1_wpb4_wg3_noprio", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": 4, "NFN_WG_PER_CU": 3, "NFN_PRIO": 0}}]
+        for wpb, wg in ((4, 1), (4, 2), (4, 3), (2, 3), (2, 5), (2, 7), (1, 12)):
+            v.append({"name": f"mem_wave1_wpb{wpb}_wg{wg}", "env": dict(A, NFN_GRAD_WAVE1=1, NFN_GRAD_WPB=wpb, NFN_WG_PER_CU=wg)})
+        for wg in (2, 3, 4, 6):
+            v.append({"name": f"mem_generic_wg{wg}", "env": dict(A, **G, NFN_WG_PER_CU=wg)})
+        v += [{"name": "generic_b", "env": dict(G)}, {"name": "wave1_wpb4_wg3_b", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": 4, "NFN_WG_PER_CU": 3}}]
+        run_grad("C2", v, rounds=4)
+        return
+    if which[0] == "gradw1occ":  # d = 1 backward: resident waves per CU, both pipelines
+        G = {"NFN_GRAD_WAVE1": 0}
+        v = [{"name": "generic", "env": dict(G)}, {"name": "generic_compute_only", "env": dict(G, NFN_ABLATE_LOADS=1)},
+             {"name": "wave1_compute_only", "env": {"NFN_GRAD_WAVE1": 1, "NFN_ABLATE_LOADS": 1}}]
+        for wpb, wgs in ((2, (4, 5, 6, 7)), (4, (2, 3)), (1, (8, 10, 12))):
+            for wg in wgs:
+                v.append({"name": f"wave1_wpb{wpb}_wg{wg}", "env": {"NFN_GRAD_WAVE1": 1, "NFN_GRAD_WPB": wpb, "NFN_WG_PER_CU": wg}})
+        for wg in (4, 5, 6):
+            v.append({"name": f"generic_wg{wg}", "env": dict(G, NFN_WG_PER_CU=wg)})
+        v.append({"name": "generic_b", "env": dict(G)})
+        run_grad("C2", v, rounds=3)
+        return
     if which[0] == "gradshape":  # the fused backward: persistent wave tiles vs one tile per workgroup
         for cfg in ("C2",):
             run_grad(cfg, [{"name": "wave_persistent", "env": {}},
