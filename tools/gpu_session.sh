@@ -125,6 +125,11 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_sq2_grad_c3 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_grad_c3" -o s2 -- \
         python3 "$ROOT/bench.py" --mode grad --config C3 --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_sq_grad)  # issue / stall breakdown of the C2 backward (two counter passes)
+      { cd /tmp; run pmc_sq1_grad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d "$OUT/pmc_sq1_grad" -o s1 -- \
+        python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+      { cd /tmp; run pmc_sq2_grad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_grad" -o s2 -- \
+        python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
     pmc_lds)  # LDS bank-conflict cycles of every bench kernel (one counter pass per mode)
       i=0
       for args in "--config C2" "--mode grad --config C2" "--config C3" "--config C5" "--mode dense_grad" "--mode dense" "--mode bijector"; do
