@@ -306,15 +306,162 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_wave1_kernel(GradArgs ga
     };
     float adj;
     // rows past B (the last tile) run on zeros; their stores fall outside the descriptors
-    const float lp = (CM == kChainPairs ? grad1_pairs(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl,
-                                                      want_lp, adj, mid)
-                                        : grad1_packed(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl,
-                                                       want_lp, adj, mid)) -
-                     corr;
+    float lp;
+    if constexpr (CM == kStaticProg) {
+      mid();
+      lp = grad1_static<kStaticTypes[0], kStaticK[0]>(z, tl + lane * S, zh, 64, P, a.trainable != 0, gl, want_lp, adj);
+    } else if constexpr (CM == kChainPairs) {
+      lp = grad1_pairs(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl, want_lp, adj, mid);
+    } else {
+      lp = grad1_packed(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl, want_lp, adj, mid);
+    }
+    lp -= corr;
     wave_lds_sync();
     flush(b0, nr, lp, norm ? f_div<true>(adj, ystd) : adj);
     wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
   }
+}
+
+// d = 1 backward with a producer / consumer workgroup (diag A/B, NFN_GRAD_PC=1): wave 0
+// STREAMS — it holds the next unit's C tiles (y, g, rows) in registers while the others
+// compute and writes them into the C LDS slots between two workgroup barriers — and waves
+// 1..C each COMPUTE one tile per unit from their slot (forward, then the reverse pass in
+// place) and store their own gradient tile, log_prob and d/dy (each prefetches its next
+// tile's y and upstream gradient itself: 2 registers).  The memory stream is then
+// issued by one wave per workgroup (the backward's loads stream fastest from few waves:
+// DESIGN "C2 backward"), the chain by C.  Every wave of a workgroup walks the same units
+// (u = blockIdx.x, + gridDim.x, ...), so both barriers are reached by all of them.
+// LDS slot j: 64 rows at the odd stride S, then the K x 64 flow inputs.
+__device__ __forceinline__ void wg_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int Q, int C, int CM>
+__global__ void __launch_bounds__(kMaxBlock, 4) chain_grad_pc_kernel(GradArgs ga) {
+  const ChainArgs& a = ga.c;
+  extern __shared__ float lds[];
+  constexpr int RSTEP = 64 / Q;
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int S = a.lds_stride;
+  const int K = a.prog.K;
+  const int P = a.P;
+  const int64_t rs = a.t_rowstride;
+  const int64_t gts = ga.gt_rowstride;
+  const int r0 = lane / Q, c4 = lane % Q;
+  const int l0 = r0 * S + 4 * c4;
+  const int slot = 64 * S + K * 64;
+  const int64_t ntiles = a.ntiles;
+  const int64_t nunits = (ntiles + C - 1) / C;
+  const int64_t ustep = gridDim.x;
+  const bool norm = a.y_mean != nullptr;
+  const bool has_g = ga.g_out != nullptr;
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int toff = (r0 * (int)rs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)rs * 4;
+  const int64_t abl_unit = a.ablate_loads ? (int64_t)blockIdx.x : -1;  // diagnostic: compute-only timing
+  if (wid == 0) {
+    // ---- streamer ----
+    float4 buf[C][Q];
+    auto issue = [&](int64_t unit) {
+      if (abl_unit >= 0) unit = abl_unit;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const int64_t b0 = (unit * C + j) * 64;
+        const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+        const auto rt = tile_rsrc(a.t + (nr > 0 ? b0 : 0) * rs, nr > 0 ? ((nr - 1) * rs + P) * 4 : 0);
+#pragma unroll
+        for (int k = 0; k < Q; ++k)
+          buf[j][k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+      }
+    };
+    int64_t unit = blockIdx.x;
+    issue(unit);
+    for (; unit < nunits; unit += ustep) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        float* tl = lds + j * slot;
+#pragma unroll
+        for (int k = 0; k < Q; ++k) {
+          float* dst = tl + l0 + k * RSTEP * S;
+          dst[0] = buf[j][k].x;
+          dst[1] = buf[j][k].y;
+          dst[2] = buf[j][k].z;
+          dst[3] = buf[j][k].w;
+        }
+      }
+      wg_lds_barrier();  // A: the unit's inputs are in the slots
+      issue(unit + ustep);  // past the end: empty descriptors
+      wg_lds_barrier();  // B: the computing waves are done with their slots
+    }
+  } else if (wid <= C) {
+    // ---- computing wave: tile (unit * C + wid - 1) from slot wid - 1 ----
+    float* tl = lds + (wid - 1) * slot;
+    float* zh = tl + 64 * S + lane;
+    float ybuf, gbuf;
+    auto issue_yg = [&](int64_t unit) {
+      if (abl_unit >= 0) unit = abl_unit;
+      const int64_t b0 = (unit * C + wid - 1) * 64;
+      const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+      const int64_t b0c = nr > 0 ? b0 : 0;
+      const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+      const auto rg = tile_rsrc(has_g ? ga.g_out + b0c : ga.g_out, has_g ? nr * 4 : 0);
+      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+      gbuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lane * 4, 0, 0));
+    };
+    const float ymean = norm ? a.y_mean[0] : 0.0f, ystd = norm ? a.y_std[0] : 1.0f;
+    const float corr = norm ? f_log<true>(ystd) : 0.0f;
+    const bool want_lp = a.out != nullptr;
+    const uint32_t types = a.prog.types[0];
+    const int goff = (r0 * (int)gts + 4 * c4) * 4;
+    const int gkstep = RSTEP * (int)gts * 4;
+    auto flush = [&](int64_t b0, int64_t nr, float lp, float gy) {
+      const int64_t no = want_lp ? nr : 0, ny = ga.grad_y ? nr : 0, nt = ga.grad_t ? nr : 0;
+      const auto ro = tile_rsrc(no > 0 ? a.out + b0 : a.out, no * 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, lp), ro, lane * 4, 0, kNT);
+      const auto rgy = tile_rsrc(ny > 0 ? ga.grad_y + b0 : ga.grad_y, ny * 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gy), rgy, lane * 4, 0, kNT);
+      const auto rgt =
+          tile_rsrc(nt > 0 ? ga.grad_t + b0 * gts : ga.grad_t, nt > 0 ? ((nt - 1) * gts + P) * 4 : 0);
+#pragma unroll
+      for (int k = 0; k < Q; ++k) {
+        const float* src = tl + l0 + k * RSTEP * S;
+        __builtin_amdgcn_raw_buffer_store_b128(f32x4{src[0], src[1], src[2], src[3]}, rgt, goff, k * gkstep, kNT);
+      }
+    };
+    issue_yg(blockIdx.x);
+    flush(0, 0, 0.0f, 0.0f);  // empty: every path into the loop ends [y, g][stores] (counted waits)
+    for (int64_t unit = blockIdx.x; unit < nunits; unit += ustep) {
+      wg_lds_barrier();  // A
+      const int64_t b0 = (unit * C + wid - 1) * 64;
+      const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+      float z = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+      const float gl = has_g ? gbuf : 1.0f;
+      issue_yg(unit + ustep);
+      float adj;
+      float lp = CM == kChainPairs
+                     ? grad1_pairs(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl, want_lp, adj)
+                     : grad1_packed(z, tl + lane * S, zh, 64, types, K, P, a.trainable != 0, gl, want_lp, adj);
+      lp -= corr;
+      wave_lds_sync();
+      flush(b0, nr, lp, norm ? f_div<true>(adj, ystd) : adj);
+      wg_lds_barrier();  // B
+    }
+  }
+}
+
+template <int Q>
+bool launch_pc_q(const GradArgs& ga, hipStream_t s, int64_t* grid) {
+  constexpr int C = 3;
+  const int cm = env_int("NFN_CHAIN_FORM", ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop);
+  auto k = cm == kChainPairs ? chain_grad_pc_kernel<Q, C, kChainPairs> : chain_grad_pc_kernel<Q, C, kChainLoop>;
+  const size_t lds = (size_t)C * (64 * ga.c.lds_stride + ga.c.prog.K * 64) * sizeof(float);
+  const int64_t nunits = (ga.c.ntiles + C - 1) / C;
+  *grid = std::max<int64_t>(1, persistent_grid(k, 64 * (C + 1), lds, nunits));
+  k<<<dim3((unsigned)*grid), dim3(64 * (C + 1)), lds, s>>>(ga);
+  return true;
 }
 
 template <int Q>
@@ -323,6 +470,8 @@ bool launch_wave1_q(const GradArgs& ga, size_t lds_block, int wpb, hipStream_t s
   auto k = cm == kChainPairs ? chain_grad_wave1_kernel<Q, kChainPairs> : chain_grad_wave1_kernel<Q, kChainLoop>;
   if (env_int("NFN_GRAD_SPLIT", 1) == 2)
     k = cm == kChainPairs ? chain_grad_wave1_kernel<Q, kChainPairs, 2> : chain_grad_wave1_kernel<Q, kChainLoop, 2>;
+  if (cm == kStaticProg && ga.c.prog.K == kStaticK[0] && ga.c.prog.types[0] == kStaticTypes[0])
+    k = chain_grad_wave1_kernel<Q, kStaticProg>;
   const int T = 64 * wpb;
   *grid = std::max<int64_t>(1, persistent_grid(k, T, lds_block, (ga.c.ntiles + wpb - 1) / wpb));
   k<<<dim3((unsigned)*grid), dim3(T), lds_block, s>>>(ga);
@@ -352,6 +501,10 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
   if constexpr (DM == 1 && FAST) {
     const int cm = env_int("NFN_CHAIN_FORM", ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop);
     if (cm == kChainPairs && env_int("NFN_GRAD_CAP", 0) != 1) k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainPairs>;
+#ifdef NFN_DIAG
+    if (cm == kStaticProg && ga.c.prog.K == kStaticK[0] && ga.c.prog.types[0] == kStaticTypes[0])
+      k = chain_grad_wave_kernel<DM, FAST, NV, 1, kStaticProg>;
+#endif
   }
   const int T = 64 * waves_per_block;
   const int64_t teams = persistent_grid(k, T, lds_block, (ga.c.ntiles + waves_per_block - 1) / waves_per_block);
@@ -395,6 +548,15 @@ bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_
   // diagnostic A/B: d = 1 fast math with 64-row tiles spanning < 2 GiB on the straight-line
   // buffer pipeline (NFN_GRAD_WAVE1=1)
   const ChainArgs& a = ga.c;
+  if (fast && dm == 1 && a.d == 1 && a.prog.K <= 16 && a.t_rowstride * 64 * 4 < ((int64_t)1 << 31) &&
+      ga.gt_rowstride * 64 * 4 < ((int64_t)1 << 31) && a.y_bstride * 64 * 4 < ((int64_t)1 << 31) &&
+      env_int("NFN_GRAD_PC", 0) == 1) {
+    switch (nv) {
+      case 2: return launch_pc_q<2>(ga, s, grid);
+      case 4: return launch_pc_q<4>(ga, s, grid);
+      case 8: return launch_pc_q<8>(ga, s, grid);
+    }
+  }
   if (fast && dm == 1 && a.d == 1 && a.prog.K <= 16 && a.t_rowstride * 64 * 4 < ((int64_t)1 << 31) &&
       ga.gt_rowstride * 64 * 4 < ((int64_t)1 << 31) && a.y_bstride * 64 * 4 < ((int64_t)1 << 31) &&
       env_int("NFN_GRAD_WAVE1", 0) == 1) {

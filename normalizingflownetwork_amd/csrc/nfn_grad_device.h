@@ -754,6 +754,13 @@ __device__ __forceinline__ float grad_sample(float (&z)[DM], float* row, float* 
   const int d = a.d;
   const int K = a.prog.K;
   float lp;
+  if constexpr (DM == 1 && FAST && CM == kStaticProg) {  // diagnostic: the C2 program at compile time
+    float a1;
+    const float lp1 = grad1_static<kStaticTypes[0], kStaticK[0]>(z[0], row, zh, zs, a.P, a.trainable != 0, gl,
+                                                                 a.out != nullptr, a1);
+    adj[0] = a1;
+    return lp1;
+  }
   if constexpr (DM == 1 && FAST) {
     if (K <= 16) {
       float a1;

@@ -67,8 +67,8 @@ def strategies():
 
 def grad_stream():
     """d = 1 backward: the straight-line buffer pipeline (chain_grad_wave1_kernel, diag
-    NFN_GRAD_WAVE1=1, in one or two prefetch pieces) against the release's generic wave
-    kernel: the same per-sample math, so log_prob, d/dt and d/dy must be bitwise equal
+    NFN_GRAD_WAVE1=1, in one or two prefetch pieces) and the producer / consumer workgroup
+    (chain_grad_pc_kernel, NFN_GRAD_PC=1) against the release's generic wave kernel: the same per-sample math, so log_prob, d/dt and d/dy must be bitwise equal
     (NaN where both are)."""
     import torch
 
@@ -88,14 +88,15 @@ def grad_stream():
         g = torch.randn((B,), generator=gen, device="cuda")
         ym, ys = (np.float32([norm[0]]), np.float32([norm[1]])) if norm else (None, None)
         outs = {}
-        for v, split in (("0", "1"), ("1", "1"), ("1", "2")):
-            os.environ["NFN_GRAD_WAVE1"], os.environ["NFN_GRAD_SPLIT"] = v, split
+        for v, split, pc in (("0", "1", "0"), ("1", "1", "0"), ("1", "2", "0"), ("0", "1", "1")):
+            os.environ["NFN_GRAD_WAVE1"], os.environ["NFN_GRAD_SPLIT"], os.environ["NFN_GRAD_PC"] = v, split, pc
             try:
-                outs[v + split] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
+                outs[v + split + pc] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
             finally:
-                os.environ.pop("NFN_GRAD_WAVE1")
-                os.environ.pop("NFN_GRAD_SPLIT")
-        for alt in ("11", "12"):
+                for k in ("NFN_GRAD_WAVE1", "NFN_GRAD_SPLIT", "NFN_GRAD_PC"):
+                    os.environ.pop(k)
+        outs["01"] = outs["010"]
+        for alt in ("110", "120", "011"):
             for a, b, what in zip(outs[alt], outs["01"], ("log_prob", "grad_t", "grad_y")):
                 same = (a == b) | (torch.isnan(a) & torch.isnan(b))
                 assert bool(same.all()), f"{ft} B={B} {alt} {what}: {int((~same).sum())} values differ"

@@ -178,6 +178,9 @@ for s in $STEPS; do
     gradc3tape) run gradc3tape 300 python tools/microbench.py gradc3tape ;;
     gradc3b128) run gradc3b128 300 python tools/microbench.py gradc3b128 ;;
     c3mem) run c3mem 300 python tools/microbench.py c3mem ;;
+    gradpc) run gradpc 400 python tools/microbench.py gradpc ;;
+    diaggrad) run diaggrad 300 python -u -m pytest tests/test_gpu_diag.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    gradstatic) run gradstatic 400 python tools/microbench.py gradstatic ;;
     gradsplit) run gradsplit 400 python tools/microbench.py gradsplit ;;
     gradw1mem) run gradw1mem 400 python tools/microbench.py gradw1mem ;;
     gradw1occ) run gradw1occ 400 python tools/microbench.py gradw1occ ;;

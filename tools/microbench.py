@@ -595,6 +595,32 @@ def main():
                            {"name": "wave1_noprio", "env": {"NFN_GRAD_WAVE1": 1, "NFN_PRIO": 0}},
                            {"name": "wave1_b", "env": {"NFN_GRAD_WAVE1": 1}}, {"name": "generic_b", "env": dict(G)}], rounds=4)
         return
+    if which[0] == "gradpc":  # d = 1 backward: producer / consumer workgroup vs the release kernel
+        PC = {"NFN_GRAD_PC": 1}
+        for cfg in ("C2", "C1"):
+            run_grad(cfg, [{"name": "release", "env": {}}, {"name": "pc", "env": dict(PC)},
+                           {"name": "pc_memory_only", "env": dict(PC, NFN_ABLATE_FLOWS=1)},
+                           {"name": "pc_compute_only", "env": dict(PC, NFN_ABLATE_LOADS=1)},
+                           {"name": "pc_wg3", "env": dict(PC, NFN_WG_PER_CU=3)},
+                           {"name": "pc_wg2", "env": dict(PC, NFN_WG_PER_CU=2)},
+                           {"name": "pc_pairs", "env": dict(PC, NFN_CHAIN_FORM=3)},
+                           {"name": "release_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                           {"name": "release_b", "env": {}}, {"name": "pc_b", "env": dict(PC)}], rounds=4)
+        return
+    if which[0] == "gradstatic":  # C2 backward: the chain program at compile time (diag) vs the runtime program
+        S = {"NFN_CHAIN_FORM": 2}
+        W = {"NFN_GRAD_WAVE1": 1}
+        v = [{"name": "loop", "env": {}}, {"name": "static", "env": dict(S)},
+             {"name": "loop_compute", "env": {"NFN_ABLATE_LOADS": 1}},
+             {"name": "static_compute", "env": dict(S, NFN_ABLATE_LOADS=1)},
+             {"name": "static_wave1", "env": dict(S, **W)},
+             {"name": "static_wave1_wpb4", "env": dict(S, **W, NFN_GRAD_WPB=4)},
+             {"name": "static_wave1_wpb1_wg12", "env": dict(S, **W, NFN_GRAD_WPB=1, NFN_WG_PER_CU=12)},
+             {"name": "static_wave1_compute", "env": dict(S, **W, NFN_ABLATE_LOADS=1)},
+             {"name": "static_wg4", "env": dict(S, NFN_WG_PER_CU=4)},
+             {"name": "loop_b", "env": {}}, {"name": "static_b", "env": dict(S)}]
+        run_grad("C2", v, rounds=4)
+        return
     if which[0] == "gradsplit":  # d = 1 backward: next-tile rows in one piece vs two (second half mid-chain)
         G = {"NFN_GRAD_WAVE1": 0}
         v = [{"name": "generic", "env": dict(G)}]
