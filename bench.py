@@ -211,7 +211,7 @@ def cpu_baseline(kind: str, cfg: str, H: int = 16, seconds: float = 8.0) -> dict
 
 def load_traffic(cfg: str, B: int):
     """Per-launch HBM bytes of the chain kernel from committed rocprofv3 PMC passes
-    (tools/pmc_traffic.py -> profiles/*pmc_<cfg>.json), or None."""
+    (`tools/prof_summary.py pmc` -> profiles/*pmc_<cfg>.json, the latest round's file), or None."""
     import glob
 
     cands = sorted(glob.glob(os.path.join(REPO, "profiles", f"*pmc_{cfg}.json")))

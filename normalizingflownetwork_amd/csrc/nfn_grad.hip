@@ -87,7 +87,8 @@ __global__ void __launch_bounds__(64) chain_grad_kernel(GradArgs ga) {
 // registers (non-temporal) while the current tile runs forward + reverse; the
 // gradient tile is then written back from LDS with coalesced non-temporal
 // float4 stores (lane -> (row, 16-byte column) as for the loads).
-template <int DM, bool FAST, int NV, int MINW, int CM = kChainLoop>
+// NTL / NTS (diag A/B only): non-temporal row loads / gradient stores (the release default).
+template <int DM, bool FAST, int NV, int MINW, int CM = kChainLoop, bool NTL = true, bool NTS = true>
 __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradArgs ga) {
   const ChainArgs& a = ga.c;
   extern __shared__ float lds[];
@@ -119,7 +120,7 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
     const float* base = a.t + b0 * rs + 4 * c4;
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      if (r0 + k * rstep < nr) buf[k] = load_row4<true>(base + (int64_t)(r0 + k * rstep) * rs);
+      if (r0 + k * rstep < nr) buf[k] = load_row4<NTL>(base + (int64_t)(r0 + k * rstep) * rs);
     if (lane < nr) {
       const float* yr = a.y + (b0 + lane) * a.y_bstride;
 #pragma unroll
@@ -175,7 +176,10 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
         if (r < nr) {
           const float* src = tl + r * S + 4 * c4;
           const f32x4 v = {src[0], src[1], src[2], src[3]};
-          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(gbase + (int64_t)r * gts));
+          if constexpr (NTS)
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(gbase + (int64_t)r * gts));
+          else
+            *reinterpret_cast<f32x4*>(gbase + (int64_t)r * gts) = v;
         }
       }
     }
@@ -504,6 +508,13 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
 #ifdef NFN_DIAG
     if (cm == kStaticProg && ga.c.prog.K == kStaticK[0] && ga.c.prog.types[0] == kStaticTypes[0])
       k = chain_grad_wave_kernel<DM, FAST, NV, 1, kStaticProg>;
+    // cache-policy A/B for the row loads and gradient stores (loop form, C2's)
+    const int ntl = env_int("NFN_GRAD_NTL", 1), nts = env_int("NFN_GRAD_NTS", 1);
+    if (cm == kChainLoop && (ntl == 0 || nts == 0)) {
+      if (ntl == 0 && nts == 0) k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainLoop, false, false>;
+      else if (ntl == 0) k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainLoop, false, true>;
+      else k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainLoop, true, false>;
+    }
 #endif
   }
   const int T = 64 * waves_per_block;

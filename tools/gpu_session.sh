@@ -130,6 +130,15 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_sq2_grad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_SMEM SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmc_sq2_grad" -o s2 -- \
         python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_all)  # FETCH_SIZE / WRITE_SIZE passes (one counter block per run) for every bench mode but the C2 forward
+      i=0
+      for args in "--mode grad --config C2" "--config C3" "--mode grad --config C3" "--config C5" "--mode dense --config C2" "--mode dense_grad --config C2" "--mode bijector --config C2"; do
+        i=$((i+1))
+        for c in FETCH_SIZE WRITE_SIZE; do
+          { cd /tmp; run pmc_all_${i}_$c 100 timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_all_${i}_$c" -o p -- \
+            python3 "$ROOT/bench.py" $args --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+        done
+      done ;;
     pmc_lds)  # LDS bank-conflict cycles of every bench kernel (one counter pass per mode)
       i=0
       for args in "--config C2" "--mode grad --config C2" "--config C3" "--config C5" "--mode dense_grad" "--mode dense" "--mode bijector"; do
@@ -178,6 +187,7 @@ for s in $STEPS; do
     gradc3tape) run gradc3tape 300 python tools/microbench.py gradc3tape ;;
     gradc3b128) run gradc3b128 300 python tools/microbench.py gradc3b128 ;;
     c3mem) run c3mem 300 python tools/microbench.py c3mem ;;
+    gradpolicy) run gradpolicy 400 python tools/microbench.py gradpolicy ;;
     gradpc) run gradpc 400 python tools/microbench.py gradpc ;;
     diaggrad) run diaggrad 300 python -u -m pytest tests/test_gpu_diag.py -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
     gradstatic) run gradstatic 400 python tools/microbench.py gradstatic ;;

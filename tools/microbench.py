@@ -595,6 +595,16 @@ def main():
                            {"name": "wave1_noprio", "env": {"NFN_GRAD_WAVE1": 1, "NFN_PRIO": 0}},
                            {"name": "wave1_b", "env": {"NFN_GRAD_WAVE1": 1}}, {"name": "generic_b", "env": dict(G)}], rounds=4)
         return
+    if which[0] == "gradpolicy":  # C2 backward: cache policy of the row loads / gradient stores
+        A = {"NFN_ABLATE_FLOWS": 1}
+        v = [{"name": "nt_nt", "env": {}}, {"name": "plainload_nt", "env": {"NFN_GRAD_NTL": 0}},
+             {"name": "nt_plainstore", "env": {"NFN_GRAD_NTS": 0}},
+             {"name": "plain_plain", "env": {"NFN_GRAD_NTL": 0, "NFN_GRAD_NTS": 0}},
+             {"name": "mem_nt_nt", "env": dict(A)}, {"name": "mem_nt_plainstore", "env": dict(A, NFN_GRAD_NTS=0)},
+             {"name": "mem_plain_plain", "env": dict(A, NFN_GRAD_NTL=0, NFN_GRAD_NTS=0)},
+             {"name": "nt_nt_b", "env": {}}, {"name": "nt_plainstore_b", "env": {"NFN_GRAD_NTS": 0}}]
+        run_grad("C2", v, rounds=4)
+        return
     if which[0] == "gradpc":  # d = 1 backward: producer / consumer workgroup vs the release kernel
         PC = {"NFN_GRAD_PC": 1}
         for cfg in ("C2", "C1"):
