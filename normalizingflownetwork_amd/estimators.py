@@ -205,6 +205,47 @@ class BaseEstimator:
                           RuntimeWarning, stacklevel=3)
         return vals[0] / n
 
+    def _get_input_model(self):
+        """``BaseEstimator.py:61-69``: ``y -> (y - mu_y) / sigma_y`` followed by Keras
+        ``GaussianNoise(y_noise_std)``, which adds noise only when called with
+        ``training=True``.  Returns ``input_model(y, training=False)`` (a device tensor)."""
+        gen = {}
+
+        def input_model(y, training=False):
+            y = ops.as_device_f32(y)
+            ym = torch.as_tensor(self.y_mean, dtype=torch.float32, device=y.device)
+            ys = torch.as_tensor(self.y_std, dtype=torch.float32, device=y.device)
+            yc = (y - ym) / ys
+            if training and self.y_noise_std > 0.0:
+                if "g" not in gen:
+                    gen["g"] = torch.Generator(device=y.device)
+                    gen["g"].manual_seed(int(self.random_seed) + 7)
+                yc = yc + self.y_noise_std * torch.randn(yc.shape, generator=gen["g"], device=y.device,
+                                                         dtype=yc.dtype)
+            return yc
+
+        return input_model
+
+    def _get_neg_log_likelihood(self):
+        """``BaseEstimator.py:55-59``: the compiled loss, ``nll(y, p_y) = -p_y.log_prob(
+        input_model(y)) + sum(log sigma_y)`` per sample (noise off: evaluation)."""
+        input_model = self._get_input_model()
+        log_sy = float(np.sum(np.log(np.asarray(self.y_std, np.float64))))
+        return lambda y, p_y: -p_y.log_prob(input_model(y)) + log_sy
+
+    def evaluate(self, x, y, batch_size=None, verbose=0, **kwargs) -> float:
+        """Keras ``Model.evaluate`` of the compiled loss (``MaximumLikelihoodNNEstimator.py:33-35``):
+        the sample mean of ``_get_neg_log_likelihood()(y, self(x))`` with noise off.  The
+        per-batch means Keras averages (weighted by batch size) equal this one mean, so the
+        data runs as one batch: the MLP in torch, ``log_prob`` in the fused chain kernel on
+        the materialised ``t`` (``score`` takes the fused Dense -> chain path: the reference's
+        ``score == -evaluate`` tests compare the two)."""
+        x = np.asarray(x, np.float32) if not isinstance(x, torch.Tensor) else x
+        y = np.asarray(y, np.float32) if not isinstance(y, torch.Tensor) else y
+        with torch.no_grad():
+            nll = self._get_neg_log_likelihood()(y, self.call(x, training=False))
+        return float(nll.double().mean().item())
+
     def _assign_noise_regularisation(self, n_dims: int, n_datapoints: int):
         """``BaseEstimator.py:33-41``."""
         assert self.noise_fn_type in ["rule_of_thumb", "fixed_rate"]
@@ -465,6 +506,19 @@ class BayesNormalizingFlowNetwork(BaseEstimator):
                     ws.append(w)
                     bs.append(b)
         return torch.stack(hs).contiguous(), torch.stack(ws).contiguous(), torch.stack(bs).contiguous()
+
+    def evaluate(self, x, y, batch_size=None, verbose=0, **kwargs) -> float:
+        """Keras ``evaluate`` of ``BayesianNNEstimator``'s compiled loss for ONE posterior
+        draw (every ``DenseVariational`` re-samples its weights per call,
+        ``BayesianNNEstimator.py:122-145``): the mean NLL of (x, y) under ``t`` of a fresh
+        draw.  The KL(q || p) regularisation term the reference adds is not mirrored
+        (SURVEY.md §2), so this is the NLL part of its loss."""
+        x = np.asarray(x, np.float32) if not isinstance(x, torch.Tensor) else x
+        y = np.asarray(y, np.float32) if not isinstance(y, torch.Tensor) else y
+        with torch.no_grad():
+            t = self.params_draws(x, 1)[0]
+            nll = self._get_neg_log_likelihood()(y, self.dist_layer(t))
+        return float(nll.double().mean().item())
 
     def params_draws(self, x, n_draws: int) -> torch.Tensor:
         """``t`` for ``n_draws`` posterior weight samples: (S, B, P)."""

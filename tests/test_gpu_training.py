@@ -208,3 +208,66 @@ def test_fit_graph_replay_matches_eager(gpu, fused, noise):
     assert out[True][0] == out[False][0]
     for a, b in zip(out[True][1], out[False][1]):
         np.testing.assert_array_equal(a, b)
+
+
+class _Wrapper:
+    def __init__(self, model):
+        self.model = model
+
+
+def test_mle_score_equals_minus_evaluate(gpu):
+    """tests/test_evaluation.py:47-55: after fitting, ``mle_log_likelihood_score`` equals
+    ``-evaluate`` (the compiled loss with noise off).  Here the two run different kernel
+    paths: the score through the fused Dense -> chain kernel with an fp64 device sum, the
+    loss through the MLP's materialised t and the chain kernel."""
+    from normalizingflownetwork_amd.scorers import mle_log_likelihood_score
+
+    x = np.linspace(-1, 1, 10).reshape((10, 1))
+    y = np.linspace(-1, 1, 10).reshape((10, 1))
+    mle = _nfn(1, n_flows=0, hidden_sizes=(6, 6), trainable_base_dist=True)
+    mle.fit(x, y, epochs=10, verbose=0)
+    assert mle_log_likelihood_score(_Wrapper(mle), x, y) == pytest.approx(-mle.evaluate(x, y), rel=1e-5)
+    # with flows, and a hidden width the fused Dense path takes (16)
+    m2 = _nfn(1, n_flows=3, hidden_sizes=(16, 16), trainable_base_dist=True)
+    m2.fit(x, y, epochs=10, verbose=0)
+    assert mle_log_likelihood_score(_Wrapper(m2), x, y) == pytest.approx(-m2.evaluate(x, y), rel=1e-5)
+
+
+def test_bayesian_score(gpu):
+    """tests/test_evaluation.py:16-44: the Bayesian scorer on a deterministic (MLE) model
+    equals ``-evaluate``; on a Bayesian model the posterior log-mean-exp score exceeds the
+    negated mean loss over 50 draws (here the loss has no KL term — SURVEY.md §2 — and the
+    inequality is Jensen's: log E[p] >= E[log p], strict while the draws differ)."""
+    from normalizingflownetwork_amd import BayesNormalizingFlowNetwork
+    from normalizingflownetwork_amd.scorers import bayesian_log_likelihood_score
+
+    rng = np.random.default_rng(22)
+    x = np.linspace(-3, 3, 300, dtype=np.float32).reshape((300, 1))
+    y = (5 * np.sin(2 * x) + np.abs(x) * rng.standard_normal((300, 1))).astype(np.float32)
+    mle = _nfn(1, n_flows=0, hidden_sizes=(6, 6), trainable_base_dist=True)
+    mle.fit(x, y, epochs=20, verbose=0)
+    mle.map_mode = False
+    assert bayesian_log_likelihood_score(_Wrapper(mle), x, y) == pytest.approx(-mle.evaluate(x, y), rel=1e-5)
+    be = BayesNormalizingFlowNetwork(n_dims=1, kl_weight_scale=1.0 / x.shape[0], n_flows=0, hidden_sizes=(6, 6),
+                                     trainable_base_dist=True)
+    be.fit(x, y, epochs=30, verbose=0)
+    score = bayesian_log_likelihood_score(_Wrapper(be), x, y)
+    loss = sum(be.evaluate(x, y) for _ in range(50)) / 50
+    assert np.isfinite(score) and score > -loss
+
+
+def test_y_noise_input_model(gpu):
+    """tests/test_noise_reg.py:50-70: with ``fixed_rate`` noise the y input model is
+    deterministic at evaluation and random while training (Keras GaussianNoise)."""
+    x = np.linspace([[-1]] * 3, [[1]] * 3, 10, dtype=np.float32).reshape((10, 3))
+    y = np.linspace([[-1]] * 3, [[1]] * 3, 10, dtype=np.float32).reshape((10, 3))
+    m = _nfn(3, n_flows=3, hidden_sizes=(16, 16), trainable_base_dist=True, noise_reg=("fixed_rate", 1.0))
+    m.fit(x, y, epochs=10, verbose=0)
+    input_model = m._get_input_model()
+    y1 = input_model(y, training=False).cpu().numpy()
+    y2 = input_model(y, training=False).cpu().numpy()
+    assert np.all(y1 == y2)
+    np.testing.assert_allclose(y1, (y - m.y_mean) / m.y_std, rtol=1e-6, atol=1e-7)
+    y1 = input_model(y, training=True).cpu().numpy()
+    y2 = input_model(y, training=True).cpu().numpy()
+    assert not np.all(y1 == y2)
