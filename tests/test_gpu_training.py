@@ -271,3 +271,37 @@ def test_y_noise_input_model(gpu):
     y1 = input_model(y, training=True).cpu().numpy()
     y2 = input_model(y, training=True).cpu().numpy()
     assert not np.all(y1 == y2)
+
+
+@pytest.mark.parametrize("d,n_flows,trainable", [(1, 3, False), (1, 0, True), (3, 3, True)])
+def test_bayes_model_output_dims(gpu, d, n_flows, trainable):
+    """tests/test_bayesian_estimator.py:23-80: after one epoch of ``fit`` the Bayesian
+    estimator's distribution has event shape [d] and batch shape [10], ``log_prob`` of a
+    broadcast row has shape [10], ``pdf`` too (1-d case), and the posterior score is finite."""
+    from normalizingflownetwork_amd import BayesNormalizingFlowNetwork
+
+    x = np.linspace([[-1]] * d, [[1]] * d, 10, dtype=np.float32).reshape((10, d))
+    m = BayesNormalizingFlowNetwork(d, kl_weight_scale=1.0 / x.shape[0], n_flows=n_flows, hidden_sizes=(16, 16),
+                                    trainable_base_dist=trainable)
+    m.fit(x, x, epochs=1, verbose=0)
+    out = m(x)
+    assert out.event_shape == [d] and out.batch_shape == [10]
+    assert tuple(out.log_prob([[0.0] * d]).shape) == (10,)
+    if d == 1:
+        assert tuple(m.pdf(x, x).shape) == (10,)
+    assert np.isfinite(m.score(x, x))
+
+
+def test_bayes_y_noise_input_model(gpu):
+    """tests/test_bayesian_estimator.py:83-106: ``rule_of_thumb`` noise on the Bayesian
+    estimator: the y input model is deterministic at evaluation, random while training."""
+    from normalizingflownetwork_amd import BayesNormalizingFlowNetwork
+
+    x = np.linspace([[-1]] * 3, [[1]] * 3, 10, dtype=np.float32).reshape((10, 3))
+    m = BayesNormalizingFlowNetwork(3, kl_weight_scale=1.0 / x.shape[0], n_flows=3, hidden_sizes=(16, 16),
+                                    trainable_base_dist=True, noise_reg=("rule_of_thumb", 1.0))
+    m.fit(x, x, epochs=10, verbose=0)
+    assert m.y_noise_std == pytest.approx(1.0 * (10 + 1) ** (-1 / (4 + 6)))
+    im = m._get_input_model()
+    assert np.all(im(x, training=False).cpu().numpy() == im(x, training=False).cpu().numpy())
+    assert not np.all(im(x, training=True).cpu().numpy() == im(x, training=True).cpu().numpy())
