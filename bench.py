@@ -14,7 +14,7 @@ all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
 resident in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
-                  [--mode forward|grad|dense|dense_grad|bijector|flows [--flow-params views|separate]]
+                  [--mode forward|grad|dense|dense_grad|bijector|flows [--flow-params views|separate|strided]]
   N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
   bench.py --gpus N), or plain `python bench.py --gpus N`, which starts that launcher as a
   child process itself (before touching the GPU) and exits with its status.
@@ -283,10 +283,12 @@ def main():
                          "step; E > 1 keeps most of the events' ~4 us per step out of the wall clock, but "
                          "then a timed launch's interval includes the dispatch gap: +1 %% at C2, "
                          "profiles/r03/r03u_event_sampling_ab.log)")
-    ap.add_argument("--flow-params", default="views", choices=["views", "separate"],
-                    help="--mode flows: the flows' parameters as views of the layer's one wide t (each "
-                         "launch reads whole 128-B rows), or built individually over their own "
-                         "contiguous (B, param_size) tensors")
+    ap.add_argument("--flow-params", default="views", choices=["views", "separate", "strided"],
+                    help="--mode flows: the flows' parameters as views of the layer's one wide t (each step "
+                         "first makes the blocks contiguous in one pass, nfn_split_blocks_f32, as the "
+                         "package's flows do), built individually over their own contiguous (B, param_size) "
+                         "tensors, or read straight from the wide rows by every launch (strided: each launch "
+                         "fetches whole 128-B lines)")
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group and run the all-reduce even at N = 1 (tests)")
     ap.add_argument("--allreduce", default="torch", choices=["torch", "native"],
@@ -340,7 +342,7 @@ def main():
         if args.mode == "bijector":
             launcher = ops.BijectorLauncher(y, t, ft, d, True)
         else:
-            launcher = ops.FlowsLauncher(y, t, ft, d, True, separate=args.flow_params == "separate")
+            launcher = ops.FlowsLauncher(y, t, ft, d, True, params=args.flow_params)
     else:
         t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device=dev)
         if grad_mode:
@@ -558,7 +560,7 @@ def main():
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense", "dense_grad": "_dense_grad",
                                                            "bijector": "_bijector",
-                                                           "flows": "_flows" if args.flow_params == "views" else "_flows_separate"
+                                                           "flows": "_flows" if args.flow_params == "views" else "_flows_" + args.flow_params
                                                            }.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -580,7 +582,8 @@ def main():
             kernel_name = "chain_wave1_kernel (Chain bijector form)" if d == 1 else "chain_fwd_ldj_kernel"
             metric = f"Chain bijector forward+fldj evals/sec (whole node), {args.config}"
         elif args.mode == "flows":
-            kernel_name = f"flow_fwd_ldj_kernel x {len(ft)} launches"
+            kernel_name = (f"flow_fwd_ldj_kernel x {len(ft)} launches"
+                           + (" after split_blocks_kernel" if args.flow_params == "views" else ""))
             metric = f"flow-by-flow bijector forward+fldj chain evals/sec (whole node), {args.config}"
         elif args.mode == "dense":
             if S is None:

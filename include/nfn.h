@@ -53,6 +53,8 @@
  *                             RadialFlow._forward/_forward_log_det_jacobian
  *                                                    estimators/normalizing_flows/RadialFlow.py:20-84
  *                             AffineFlow (tfp Affine) estimators/normalizing_flows/AffineFlow.py:4-9
+ *   nfn_split_blocks_f32   <- the tf slices t[:, o:o+size] (copies) that _get_bijector hands each
+ *                             flow                   estimators/DistributionLayers.py:267-278
  *   nfn_chain_fwd_ldj_f32  <- tfp Chain(flows).forward / .forward_log_det_jacobian as composed by
  *                             InverseNormalizingFlowLayer._get_bijector
  *                                                    estimators/DistributionLayers.py:267-278
@@ -96,11 +98,12 @@ extern "C" {
 #define NFN_COMM_ID_BYTES 128
 
 /* Library version as MAJOR*10000 + MINOR*100 + PATCH.
+ *   201 (0.2.1): + nfn_split_blocks_f32 (additive; every 200 entry point unchanged).
  *   200 (0.2.0): out_sum is a device double[2] {sum, non-finite count} (was double[1]);
  *                the workspace needs no initialisation (its finishing ticket carries a
  *                per-call epoch).
  *   100 (0.1.0): first release. */
-#define NFN_ABI_VERSION 200
+#define NFN_ABI_VERSION 201
 int32_t nfn_version(void);
 
 /* Message of the last failing call on this thread ("" if none). */
@@ -219,6 +222,20 @@ int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32
 int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
                              int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out,
                              void* stream);
+
+/*
+ * Column blocks of a parameter row, each made contiguous, in ONE pass over t:
+ *   t      : (B, >= sum(widths)) rows at t_rowstride floats; block k is the widths[k]
+ *            columns after blocks 0..k-1 (t points at block 0's first column)
+ *   dst    : block k lands at dst + B * (widths[0] + ... + widths[k-1]) as a contiguous
+ *            (B, widths[k]) array; dst must not overlap t
+ * What InverseNormalizingFlowLayer._get_bijector's slices t[:, o:o+size] are in TF — copies
+ * (estimators/DistributionLayers.py:267-278): the per-flow Bijector calls then read only their
+ * own parameters (nfn_flow_fwd_ldj_f32 on a view of the wide row reads the whole 128-B lines).
+ * 1 <= nblocks <= NFN_MAX_FLOWS, widths[k] >= 1.
+ */
+int32_t nfn_split_blocks_f32(const float* t, int64_t t_rowstride, int64_t B, const int32_t* widths, int32_t nblocks,
+                             float* dst, void* stream);
 
 /*
  * The Bijector API's Chain of flows in ONE launch (instead of one launch per flow):

@@ -914,6 +914,35 @@ int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride,
   return check_hip("flow_fwd_ldj_kernel launch");
 }
 
+int32_t nfn_split_blocks_f32(const float* t, int64_t t_rowstride, int64_t B, const int32_t* widths, int32_t nblocks,
+                             float* dst, void* stream) {
+  g_last_error.clear();
+  if (nblocks < 1 || nblocks > NFN_MAX_FLOWS) return fail(NFN_E_SHAPE, "nblocks must be in [1, " + std::to_string(NFN_MAX_FLOWS) + "]");
+  if (!widths) return fail(NFN_E_NULLPTR, "widths is NULL");
+  if (B < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
+  SplitArgs sa;
+  memset(&sa, 0, sizeof(sa));
+  int64_t W = 0;
+  for (int32_t k = 0; k < nblocks; ++k) {
+    if (widths[k] < 1) return fail(NFN_E_SHAPE, "block widths must be >= 1");
+    sa.widths[k] = widths[k];
+    W += widths[k];
+  }
+  if (W > 1024) return fail(NFN_E_SHAPE, "blocks wider than 1024 floats in total");
+  if (B > 1 && t_rowstride < W) return fail(NFN_E_SHAPE, "t row stride < the blocks' total width");
+  if (B == 0) return NFN_OK;
+  if (!t || !dst) return fail(NFN_E_NULLPTR, "t or dst is NULL");
+  if (B > (int64_t)0x7fffffff) return fail(NFN_E_SHAPE, "batch too large");
+  sa.t = t;
+  sa.rs = t_rowstride;
+  sa.B = B;
+  sa.dst = dst;
+  sa.W = (int32_t)W;
+  sa.nblocks = nblocks;
+  launch_split_blocks(sa, reinterpret_cast<hipStream_t>(stream));
+  return check_hip("split_blocks_kernel launch");
+}
+
 int32_t nfn_chain_fwd_ldj_f32(const float* z, int64_t z_bstride, const float* t, int64_t t_rowstride, int64_t B,
                               int32_t d, const int32_t* flow_ids, const int32_t* block_offsets, int32_t K,
                               float* z_out, float* ldj_out, void* stream) {

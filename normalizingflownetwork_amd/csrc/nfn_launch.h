@@ -139,6 +139,16 @@ void launch_sample(bool fast, int dm, const SampleArgs& sa, dim3 grid, dim3 bloc
 // nfn_grid.hip
 void launch_grid(bool fast, int dm, const GridArgs& ga, dim3 grid, dim3 block, size_t lds, hipStream_t s);
 // nfn_misc.hip
+struct SplitArgs {
+  const float* t;
+  int64_t rs;  // row stride of t (floats)
+  int64_t B;
+  float* dst;
+  int32_t W;  // sum of the widths
+  int32_t nblocks;
+  int32_t widths[NFN_MAX_FLOWS];
+};
+void launch_split_blocks(const SplitArgs& sa, hipStream_t s);
 void launch_reduce_partials(const double* ws, double* out, hipStream_t s);
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s);
 void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,

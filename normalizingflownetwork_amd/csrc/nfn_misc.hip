@@ -34,7 +34,77 @@ __global__ void __launch_bounds__(1024) reduce_f64_kernel(const double* __restri
   if (threadIdx.x == 0) out[0] = s;
 }
 
+// nfn_split_blocks_f32: one workgroup per R-row tile.  When the rows are dense (row stride
+// rs at most W + 32 floats: the gap columns share the blocks' cache lines, so reading them
+// costs no HBM bytes) the tile's whole span [row0 * rs, (row0 + R - 1) * rs + W) is read as
+// 16-byte buffer loads, every lane active, from the 16-byte-aligned address at or below its
+// first float (`mis` floats lower; the descriptor is bounded at the last valid float, so
+// nothing outside t is read); otherwise row by row (one row's W dwords per wave
+// instruction).  The tile goes to LDS, then each block is written as its own contiguous
+// (rows x w) run, lanes over consecutive floats (row = e / w by a float reciprocal: e <
+// 2^18, so the quotient never rounds across an integer).  R * (span of a row) <= 16384
+// floats: 64 KiB of LDS.
+constexpr int kSplitTileFloats = 16384;
+
+__host__ __device__ inline bool split_dense(int64_t rs, int W) { return rs <= (int64_t)W + 32; }
+
+__host__ __device__ inline int split_rows(int64_t rs, int W) {
+  const int64_t span = split_dense(rs, W) ? max(rs, (int64_t)W) : (int64_t)W;
+  return (int)max((int64_t)4, min((int64_t)256, ((kSplitTileFloats - 8) / span) & ~(int64_t)3));
+}
+
+__global__ void __launch_bounds__(256) split_blocks_kernel(SplitArgs sa) {
+  extern __shared__ float tile[];
+  const int W = sa.W;
+  const int64_t rs = sa.rs;
+  const bool dense = split_dense(rs, W);
+  const int R = split_rows(rs, W);
+  const int64_t b0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min((int64_t)R, sa.B - b0);
+  int mis = 0;       // floats between the aligned load base and the tile's first float
+  int64_t lrs = W;   // row stride of the LDS tile
+  if (dense) {
+    mis = (int)((reinterpret_cast<uintptr_t>(sa.t) & 15) >> 2);
+    lrs = max(rs, (int64_t)W);
+    const float* base = sa.t + b0 * rs - mis;  // 16-byte aligned: R * rs * 4 is a multiple of 16
+    const int n = mis + (int)((nr - 1) * lrs) + W;  // floats of the tile's span from base
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, n * 4, 0x00020000);
+    float4* t4 = reinterpret_cast<float4*>(tile);
+    for (int v = threadIdx.x; v < (n + 3) / 4; v += blockDim.x)
+      t4[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, v * 16, 0, 2));
+  } else {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int r = wid; r < nr; r += nw) {
+      const float* row = sa.t + (b0 + r) * rs;
+      for (int c = lane; c < W; c += 64) tile[r * W + c] = __builtin_nontemporal_load(row + c);
+    }
+  }
+  __syncthreads();
+  int off = mis;
+  int64_t dofs = 0;
+  for (int k = 0; k < sa.nblocks; ++k) {
+    const int w = sa.widths[k];
+    const float rw = 1.0f / (float)w;
+    float* dst = sa.dst + dofs + b0 * w;
+    const int n = nr * w;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int r = (int)(((float)e + 0.5f) * rw);
+      __builtin_nontemporal_store(tile[r * lrs + off + (e - r * w)], dst + e);
+    }
+    off += w;
+    dofs += sa.B * w;
+  }
+}
+
 }  // namespace
+
+void launch_split_blocks(const SplitArgs& sa, hipStream_t s) {
+  const int R = split_rows(sa.rs, sa.W);
+  const int64_t span = split_dense(sa.rs, sa.W) ? std::max<int64_t>(sa.rs, sa.W) : sa.W;
+  const size_t lds = (size_t)(R * span + 8) * sizeof(float);  // + the aligned span's up to 5 extra floats
+  const int64_t nblk = (sa.B + R - 1) / R;
+  hipLaunchKernelGGL(split_blocks_kernel, dim3((unsigned)nblk), dim3(256), lds, s, sa);
+}
 
 void launch_reduce_partials(const double* ws, double* out, hipStream_t s) {
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, s, ws, out);

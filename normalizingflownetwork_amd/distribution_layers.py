@@ -19,6 +19,7 @@ import torch
 
 from . import ops
 from .normalizing_flows import FLOWS, Chain, Invert
+from .normalizing_flows.flows import SplitBlocks
 
 
 class TensorShape(tuple):
@@ -261,6 +262,12 @@ class InverseNormalizingFlowLayer:
         for size, flow_type in zip(param_sizes, flow_types):
             chain.append(FLOWS[flow_type](_cols(t, begin, begin + size), n_dims))
             begin += size
+        if isinstance(t, torch.Tensor) and t.dim() == 2 and t.stride(-1) == 1 and len(chain) > 1:
+            # the flows' own launches read contiguous copies of their blocks, made in one
+            # pass on the first such call (TF's slices are copies; normalizing_flows.SplitBlocks)
+            group = SplitBlocks(t, param_sizes)
+            for k, f in enumerate(chain):
+                f._split = (group, k)
         return Chain(chain)
 
     @staticmethod

@@ -16,6 +16,8 @@ are moved to the HIP device.  Outputs are float32 device tensors.
 
 from __future__ import annotations
 
+import torch
+
 from .. import ops
 from .bijector import Bijector
 
@@ -29,6 +31,30 @@ def _width(t) -> int:
     return int(shape[-1])
 
 
+class SplitBlocks:
+    """The contiguous copies of consecutive column blocks of one parameter tensor, made in
+    ONE pass (``ops.split_blocks`` -> ``nfn_split_blocks_f32``) on first use and shared by the
+    flows that hold views of those blocks.  TF's ``t[:, o:o+size]`` slices in
+    ``_get_bijector`` (``DistributionLayers.py:267-278``) ARE such copies; here they are made
+    only when a flow is called on its own (the one-launch Chain reads the wide rows
+    directly), and remade if ``base`` was modified in place since (torch version counter).
+    Why: a single-flow launch over a view of the wide rows fetches each row's whole 128-B
+    lines for its few parameters (per-flow Bijector)."""
+
+    def __init__(self, base, widths):
+        self.base = base
+        self.widths = [int(w) for w in widths]
+        self._blocks = None
+        self._version = None
+
+    def blocks(self):
+        ver = self.base._version
+        if self._blocks is None or self._version != ver:
+            self._blocks = ops.split_blocks(self.base, self.widths)
+            self._version = ver
+        return self._blocks
+
+
 class _ConditionedFlow(Bijector):
     flow_type: str = ""
 
@@ -37,6 +63,7 @@ class _ConditionedFlow(Bijector):
         assert _width(t) == self.get_param_size(n_dims)
         self.n_dims = int(n_dims)
         self._t = t  # raw Dense output block; moved to the device on first use
+        self._split = None  # (SplitBlocks, index): set by InverseNormalizingFlowLayer._get_bijector
 
     @property
     def params(self):
@@ -45,17 +72,27 @@ class _ConditionedFlow(Bijector):
             self._t = ops.as_device_f32(self._t)
         return self._t
 
+    def _kernel_params(self):
+        """The block this flow's own launch reads: its contiguous copy when the flow holds a
+        strided view of a wider row that belongs to a split group, else ``params``."""
+        t = self.params
+        if (self._split is not None and t.dim() == 2 and t.shape[0] > 1 and t.stride(0) != t.shape[1]
+                and not (torch.is_grad_enabled() and t.requires_grad)):
+            group, k = self._split
+            return group.blocks()[k]
+        return t
+
     def _forward(self, z):
-        z_out, _ = ops.flow_forward_ldj(self.flow_type, z, self.params, self.n_dims, want_ldj=False)
+        z_out, _ = ops.flow_forward_ldj(self.flow_type, z, self._kernel_params(), self.n_dims, want_ldj=False)
         return z_out
 
     def _forward_log_det_jacobian(self, z):
-        _, ldj = ops.flow_forward_ldj(self.flow_type, z, self.params, self.n_dims, want_z=False)
+        _, ldj = ops.flow_forward_ldj(self.flow_type, z, self._kernel_params(), self.n_dims, want_z=False)
         return ldj
 
     def forward_and_log_det_jacobian(self, z):
         """Both results from one kernel launch."""
-        return ops.flow_forward_ldj(self.flow_type, z, self.params, self.n_dims)
+        return ops.flow_forward_ldj(self.flow_type, z, self._kernel_params(), self.n_dims)
 
 
 class PlanarFlow(_ConditionedFlow):

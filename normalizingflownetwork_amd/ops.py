@@ -626,6 +626,26 @@ def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, w
     return z_out, ldj
 
 
+def split_blocks(t: torch.Tensor, widths: Sequence[int]):
+    """``[t[:, o_k:o_k + w_k].contiguous() for each block]`` in ONE pass over ``t``
+    (``nfn_split_blocks_f32``): ``t`` (B, >= sum(widths)) device rows with unit column
+    stride, the blocks consecutive from column 0.  The blocks are views of one allocation.
+    What the TF slices of ``_get_bijector`` are (``DistributionLayers.py:267-278``: copies)."""
+    assert isinstance(t, torch.Tensor) and t.dim() == 2 and t.stride(1) == 1, "t must be (B, W), unit column stride"
+    widths = [int(w) for w in widths]
+    B, W = int(t.shape[0]), sum(widths)
+    assert t.shape[1] >= W, "t narrower than its blocks"
+    buf = torch.empty((B * W,), dtype=torch.float32, device=t.device)
+    arr = (ctypes.c_int32 * max(1, len(widths)))(*widths)
+    rc = _lib.load().nfn_split_blocks_f32(_ptr(t), _row_stride(t), B, arr, len(widths), _ptr(buf), _stream())
+    _lib.check(rc, "nfn_split_blocks_f32")
+    out, off = [], 0
+    for w in widths:
+        out.append(buf[off:off + B * w].view(B, w))
+        off += B * w
+    return out
+
+
 def chain_forward_ldj(flow_types: Sequence[str], z, t, block_offsets: Sequence[int], n_dims: int,
                       want_z: bool = True, want_ldj: bool = True):
     """A Chain of flows as ONE kernel launch (``nfn_chain_fwd_ldj_f32``): ``(z_K, sum_k
@@ -743,25 +763,33 @@ class BijectorLauncher:
 class FlowsLauncher:
     """Pre-bound flow-by-flow Bijector path for the benchmark: the Chain's K flows as K
     single-flow launches (``nfn_flow_fwd_ldj_f32``, PlanarFlow.py:68-80 / RadialFlow.py:50-70 /
-    AffineFlow.py called one bijector at a time), each reading its own block of every row
-    of ``t`` (the layer's reversed layout) and the previous flow's z, writing z and its own
-    log|det J| (``ldj`` (K, B)).  ``z_out`` holds z_K after ``launch()``.
+    AffineFlow.py called one bijector at a time), flow k reading its own parameters and the
+    previous flow's z, writing z and its own log|det J| (``ldj`` (K, B)).  ``z_out`` holds
+    z_K after ``launch()``.  ``params`` says where the parameters come from:
 
-    ``separate=True``: the flows are built individually, each over its own contiguous
-    (B, param_size) parameter tensor (copied from its block of ``t`` here, once), instead of
-    as views of the one wide ``t`` — the case where a launch reads only its own bytes."""
+    * ``"views"`` (what ``normalizing_flows`` does for the flows of one layer's ``t``): each
+      ``launch()`` first makes the flows' blocks contiguous in ONE pass over ``t``
+      (``nfn_split_blocks_f32``, as TF's slices copy them), then runs the K launches on the
+      contiguous blocks;
+    * ``"separate"``: the flows were built individually, each over its own contiguous
+      (B, param_size) tensor (copied here, once, outside the timed launches);
+    * ``"strided"``: each launch reads its block straight from the wide rows of ``t``
+      (every launch then fetches the whole 128-B lines: the pre-split path, for the record)."""
 
     def __init__(self, z: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
-                 trainable_base: bool, separate: bool = False):
+                 trainable_base: bool, separate: bool = False, params: Optional[str] = None):
         self.lib = _lib.load()
         dev = z.device
         d = int(n_dims)
+        self.mode = params or ("separate" if separate else "views")
+        assert self.mode in ("views", "separate", "strided")
         P = total_param_size(flow_types, d, trainable_base)
         assert z.dim() == 2 and z.shape[1] == d and z.stride(1) == 1
         assert t.dim() == 2 and t.shape[1] == P and t.stride(1) == 1
         B = max(int(z.shape[0]), int(t.shape[0]))
         self.B, K = B, len(flow_types)
-        off, offs = 2 * d if trainable_base else 0, [0] * K
+        base = 2 * d if trainable_base else 0
+        off, offs = base, [0] * K
         for k in reversed(range(K)):
             offs[k] = off
             off += param_size(flow_types[k], d)
@@ -769,16 +797,26 @@ class FlowsLauncher:
         self.ldj = torch.empty((max(1, K), B), dtype=torch.float32, device=dev)
         self.z_out = zs[(K - 1) % 2] if K else z
         self._calls = []
-        self.params = []  # separate=True: the flows' own parameter tensors (kept alive here)
+        self._split = None
+        self.params = []  # the flows' contiguous parameter tensors (kept alive here)
+        if self.mode != "strided" and K:
+            # blocks in row order: flow K-1 first (the layer's reversed layout)
+            order = sorted(range(K), key=lambda k: offs[k])
+            widths = [param_size(flow_types[k], d) for k in order]
+            tb = t[:, base:]
+            blocks = split_blocks(tb, widths)
+            if self.mode == "views":
+                self._split = (_ptr(tb), _row_stride(tb), B, (ctypes.c_int32 * len(widths))(*widths), len(widths),
+                               _ptr(blocks[0]))
+            by_flow = {k: blocks[i] for i, k in enumerate(order)}
+            self.params = [by_flow[k] for k in range(K)]
         zin = z
         for k, f in enumerate(flow_types):
             zo = zs[k % 2]
-            if separate:
-                pk = t[:, offs[k]:offs[k] + param_size(f, d)].contiguous()
-                self.params.append(pk)
-                pptr, pstride = _ptr(pk), _row_stride(pk)
-            else:
+            if self.mode == "strided":
                 pptr, pstride = _ptr(t) + 4 * offs[k], _row_stride(t)
+            else:
+                pptr, pstride = _ptr(self.params[k]), param_size(f, d)
             self._calls.append((FLOW_IDS[f], _ptr(zin), _row_stride(zin), pptr, pstride, B, d, _ptr(zo),
                                 _ptr(self.ldj[k])))
             zin = zo
@@ -786,6 +824,10 @@ class FlowsLauncher:
 
     def launch(self, stream: Optional[int] = None) -> None:
         st = stream if stream is not None else _stream()
+        if self._split is not None:
+            rc = self.lib.nfn_split_blocks_f32(*self._split, st)
+            if rc != 0:
+                _lib.check(rc, "nfn_split_blocks_f32")
         for args in self._calls:
             rc = self.lib.nfn_flow_fwd_ldj_f32(*args, st)
             if rc != 0:

@@ -44,12 +44,13 @@ def test_exported_symbols_are_c_linkage(native_lib):
 
 
 def test_version(native_lib):
-    # 200: out_sum is double[2] and the workspace needs no initialisation (include/nfn.h)
+    # 200: out_sum is double[2] and the workspace needs no initialisation; 201: + the
+    # additive nfn_split_blocks_f32 (include/nfn.h)
     from normalizingflownetwork_amd import _lib
 
-    assert native_lib.nfn_version() == _lib.ABI_VERSION == 200
+    assert native_lib.nfn_version() == _lib.ABI_VERSION == 201
     hdr = open(os.path.join(REPO, "include", "nfn.h")).read()
-    assert re.search(r"#define NFN_ABI_VERSION 200\b", hdr)
+    assert re.search(r"#define NFN_ABI_VERSION 201\b", hdr)
 
 
 def _ids(*names):
@@ -176,3 +177,19 @@ def test_dense_entry_point_validates(native_lib):
     assert f(*args(16, 8)) == _lib.NFN_E_SHAPE        # row stride < H
     assert f(*args(16, 18)) == _lib.NFN_E_SHAPE       # row stride not a multiple of 4
     assert "dense" in _lib.last_error() or "stride" in _lib.last_error()
+
+
+def test_split_blocks_entry_point_validates(native_lib):
+    from normalizingflownetwork_amd import _lib
+
+    f = native_lib.nfn_split_blocks_f32
+    w3 = (ctypes.c_int32 * 3)(3, 3, 2)
+    p_w = ctypes.cast(w3, ctypes.c_void_p)
+    assert f(None, 8, 10, p_w, 3, None, None) == _lib.NFN_E_NULLPTR      # t / dst NULL
+    assert f(None, 8, 10, None, 3, None, None) == _lib.NFN_E_NULLPTR     # widths NULL
+    assert f(None, 8, 10, p_w, 0, None, None) == _lib.NFN_E_SHAPE        # no blocks
+    assert f(None, 7, 10, p_w, 3, None, None) == _lib.NFN_E_SHAPE        # row stride < 8
+    assert "stride" in _lib.last_error()
+    w0 = (ctypes.c_int32 * 2)(3, 0)
+    assert f(None, 8, 10, ctypes.cast(w0, ctypes.c_void_p), 2, None, None) == _lib.NFN_E_SHAPE
+    assert f(None, 8, 0, p_w, 3, None, None) == _lib.NFN_OK              # empty batch: nothing to do

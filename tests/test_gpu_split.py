@@ -1,0 +1,78 @@
+"""The per-flow Bijector path over the views ``InverseNormalizingFlowLayer._get_bijector``
+hands each flow (``estimators/DistributionLayers.py:267-278``): the flows' blocks are made
+contiguous in ONE pass (``nfn_split_blocks_f32``; TF's slices are copies) on the first
+single-flow call, and every flow's launch reads its own copy.  Checked bitwise against the
+same launches on torch-made contiguous copies and on the strided views, with the cache
+remade after an in-place change of ``t``."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("widths,B,extra,col0", [([3] * 10, 4099, 0, 2), ([16] + [17] * 4 + [10] * 4, 1000, 0, 16),
+                                                 ([65] * 5, 333, 0, 0), ([3, 3], 1, 0, 2), ([2, 5, 1], 257, 7, 1),
+                                                 ([3, 3], 300, 100, 3), ([3] * 10, (1 << 20) + 3, 0, 2)])
+def test_split_blocks_equals_slices(gpu, widths, B, extra, col0):
+    """Dense rows (the 16-byte span loads, 0-3 floats of misalignment) and sparse rows
+    (stride > W + 32: row-by-row loads), ragged batches, one row."""
+    from normalizingflownetwork_amd import ops
+
+    W = sum(widths)
+    gen = torch.Generator(device=gpu).manual_seed(B + W)
+    wide = torch.randn((B, W + extra + col0), generator=gen, device=gpu)
+    t = wide[:, col0:col0 + W]  # a column view of a wider row (stride W + extra + col0)
+    got = ops.split_blocks(t, widths)
+    off = 0
+    for w, blk in zip(widths, got):
+        assert blk.shape == (B, w) and blk.is_contiguous()
+        assert torch.equal(blk, t[:, off:off + w].contiguous())
+        off += w
+
+
+def _layer_flows(ft, d, t):
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+
+    return InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d).bijectors
+
+
+@pytest.mark.parametrize("ft,d,B", [(("planar", "radial") * 5, 1, 5000), (("affine", "planar", "radial"), 3, 777)])
+def test_per_flow_calls_read_split_copies(gpu, ft, d, B):
+    from normalizingflownetwork_amd import ops
+    from normalizingflownetwork_amd.normalizing_flows import FLOWS
+
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device=gpu).manual_seed(B)
+    t = torch.randn((B, P), generator=gen, device=gpu)
+    z0 = torch.randn((B, d), generator=gen, device=gpu)
+    flows = _layer_flows(ft, d, t)
+    group = flows[0]._split[0]
+    assert all(f._split[0] is group for f in flows)
+
+    def run(fs):
+        z, out = z0, []
+        for f in reversed(fs):  # bijectors[-1] applies first (tfp Chain)
+            z, l = f.forward_and_log_det_jacobian(z)
+            out.append((z.clone(), l.clone()))
+        return out
+
+    got = run(flows)
+    blocks = group.blocks()
+    assert all(f._kernel_params().data_ptr() == blocks[k].data_ptr() for k, f in enumerate(flows))
+    ref_copy = run([FLOWS[type(f).flow_type](f.params.contiguous(), d) for f in flows])
+    ref_view = run([FLOWS[type(f).flow_type](f.params, d) for f in flows])
+    for (zg, lg), (zc, lc), (zv, lv) in zip(got, ref_copy, ref_view):
+        assert torch.equal(zg, zc) and torch.equal(lg, lc)
+        assert torch.equal(zg, zv) and torch.equal(lg, lv)
+    # the split is made once and reused while t is unchanged
+    assert group.blocks()[0] is blocks[0]
+    # an in-place change of t is seen: the copies are remade
+    t.mul_(0.5)
+    got2 = run(flows)
+    assert group.blocks()[0] is not blocks[0]
+    ref2 = run([FLOWS[type(f).flow_type](f.params.contiguous(), d) for f in flows])
+    for (zg, lg), (zc, lc) in zip(got2, ref2):
+        assert torch.equal(zg, zc) and torch.equal(lg, lc)
+    assert not torch.equal(got2[-1][1], got[-1][1])
