@@ -139,6 +139,15 @@ for s in $STEPS; do
             python3 "$ROOT/bench.py" $args --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
         done
       done ;;
+    pmc_dma)  # C2 forward, register hand-off vs LDS-DMA row fill (diag build): HBM bytes + SQ counters per variant
+      for v in regs dma; do
+        if [ $v = dma ]; then K=NFN_WAVE1_DMA=1; else K=NFN_WAVE1_DMA=0; fi
+        for c in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" "SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA"; do
+          tag=$(echo $c | cut -d' ' -f1)
+          { cd /tmp; run pmc_dma_${v}_$tag 100 timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_dma_${v}_$tag" -o p -- \
+            python3 "$ROOT/tools/run_variant.py" C2 $K --launches 5; cd "$ROOT"; }
+        done
+      done ;;
     pmc_lds)  # LDS bank-conflict cycles of every bench kernel (one counter pass per mode)
       i=0
       for args in "--config C2" "--mode grad --config C2" "--config C3" "--config C5" "--mode dense_grad" "--mode dense" "--mode bijector"; do

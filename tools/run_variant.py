@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Launch one config's forward kernel a few times under a diagnostic-build knob (for
+rocprofv3 --pmc passes over a single variant: run it as the program after `--`).
+
+  python3 tools/run_variant.py C2 NFN_WAVE1_DMA=1 [--launches 5]"""
+
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cfg")
+    ap.add_argument("knobs", nargs="*", help="NAME=VALUE diagnostic-build knobs")
+    ap.add_argument("--launches", type=int, default=5)
+    a = ap.parse_args()
+    cfg, knobs, n = a.cfg, dict(k.split("=", 1) for k in a.knobs), a.launches
+    os.environ.update(knobs)  # read by the diag library at each launch
+    import torch
+
+    from normalizingflownetwork_amd import _lib
+
+    _lib.use_diagnostic_build()
+    from normalizingflownetwork_amd import ops
+    from tools.microbench import CFG
+
+    ft, d, B, S = CFG[cfg]
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(1)
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device="cuda")
+    L = ops.ChainLauncher(y, t, ft, d, True, draws=S)
+    for _ in range(n):
+        L.launch()
+    torch.cuda.synchronize()
+    print({"cfg": cfg, "knobs": knobs, "launches": n, "mean_log_prob": float(L.out.double().mean().item())})
+
+
+if __name__ == "__main__":
+    main()
