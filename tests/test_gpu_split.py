@@ -76,3 +76,23 @@ def test_per_flow_calls_read_split_copies(gpu, ft, d, B):
     for (zg, lg), (zc, lc) in zip(got2, ref2):
         assert torch.equal(zg, zc) and torch.equal(lg, lc)
     assert not torch.equal(got2[-1][1], got[-1][1])
+
+
+def test_one_launch_chain_makes_no_copies(gpu):
+    """The Chain's one-launch path reads the wide rows directly: calling it leaves the
+    layer's split group empty (no 2 B-per-parameter copy is made unless a flow is called
+    on its own)."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer, ops
+
+    ft, d, B = ("planar", "radial") * 3, 1, 3000
+    P = ops.total_param_size(ft, d, True)
+    gen = torch.Generator(device=gpu).manual_seed(7)
+    t = torch.randn((B, P), generator=gen, device=gpu)
+    z = torch.randn((B, d), generator=gen, device=gpu)
+    chain = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d)
+    assert chain._fused() is not None
+    chain.forward(z)
+    chain.forward_log_det_jacobian(z, event_ndims=1)
+    assert chain.bijectors[0]._split[0]._blocks is None
+    chain.bijectors[-1].forward(z)  # a single flow on its own: now the copies exist
+    assert chain.bijectors[0]._split[0]._blocks is not None
