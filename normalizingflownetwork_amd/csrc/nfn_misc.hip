@@ -87,10 +87,21 @@ __global__ void __launch_bounds__(256) split_blocks_kernel(SplitArgs sa) {
     const float rw = 1.0f / (float)w;
     float* dst = sa.dst + dofs + b0 * w;
     const int n = nr * w;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    auto at = [&](int e) {
       const int r = (int)(((float)e + 0.5f) * rw);
-      __builtin_nontemporal_store(tile[r * lrs + off + (e - r * w)], dst + e);
+      return tile[r * lrs + off + (e - r * w)];
+    };
+    int e0 = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {  // 16-byte stores for the run's whole float4s
+      const int n4 = n >> 2;
+      for (int q = threadIdx.x; q < n4; q += blockDim.x) {
+        const int e = 4 * q;
+        const f32x4 v = {at(e), at(e + 1), at(e + 2), at(e + 3)};
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst + e));
+      }
+      e0 = 4 * n4;
     }
+    for (int e = e0 + threadIdx.x; e < n; e += blockDim.x) __builtin_nontemporal_store(at(e), dst + e);
     off += w;
     dofs += sa.B * w;
   }
