@@ -47,8 +47,17 @@ class SplitBlocks:
         self._blocks = None
         self._version = None
 
+    def version(self):
+        """The base tensor's in-place version counter, or None for a tensor that has none
+        (made under ``torch.inference_mode()``): its copies could not be validated, so
+        the flows then read the wide rows directly."""
+        try:
+            return self.base._version
+        except RuntimeError:
+            return None
+
     def blocks(self):
-        ver = self.base._version
+        ver = self.version()
         if self._blocks is None or self._version != ver:
             self._blocks = ops.split_blocks(self.base, self.widths)
             self._version = ver
@@ -79,7 +88,8 @@ class _ConditionedFlow(Bijector):
         if (self._split is not None and t.dim() == 2 and t.shape[0] > 1 and t.stride(0) != t.shape[1]
                 and not (torch.is_grad_enabled() and t.requires_grad)):
             group, k = self._split
-            return group.blocks()[k]
+            if group.version() is not None:
+                return group.blocks()[k]
         return t
 
     def _forward(self, z):

@@ -96,3 +96,24 @@ def test_one_launch_chain_makes_no_copies(gpu):
     assert chain.bijectors[0]._split[0]._blocks is None
     chain.bijectors[-1].forward(z)  # a single flow on its own: now the copies exist
     assert chain.bijectors[0]._split[0]._blocks is not None
+
+
+def test_inference_mode_tensor_reads_wide_rows(gpu):
+    """A ``t`` made under ``torch.inference_mode()`` has no version counter, so its copies
+    could not be checked against in-place changes: the flows then read the wide rows
+    directly (the same values, no copies)."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer, ops
+    from normalizingflownetwork_amd.normalizing_flows import FLOWS
+
+    ft, d, B = ("planar", "radial") * 2, 1, 2000
+    P = ops.total_param_size(ft, d, True)
+    with torch.inference_mode():
+        gen = torch.Generator(device=gpu).manual_seed(8)
+        t = torch.randn((B, P), generator=gen, device=gpu)
+        z = torch.randn((B, d), generator=gen, device=gpu)
+        flows = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d).bijectors
+        f = flows[0]
+        zg, lg = f.forward_and_log_det_jacobian(z)
+        assert f._split[0]._blocks is None and f._kernel_params().data_ptr() == f.params.data_ptr()
+        zc, lc = FLOWS[type(f).flow_type](f.params.contiguous(), d).forward_and_log_det_jacobian(z)
+        assert torch.equal(zg, zc) and torch.equal(lg, lc)
