@@ -147,7 +147,7 @@ def test_comm_entry_points_validate_before_rccl(native_lib):
     assert native_lib.nfn_comm_init(ctypes.byref(h), 2, p_uid, 2) == _lib.NFN_E_SHAPE
     assert native_lib.nfn_comm_init(ctypes.byref(h), 2, None, 0) == _lib.NFN_E_NULLPTR
     assert native_lib.nfn_comm_unique_id(None) == _lib.NFN_E_NULLPTR
-    assert native_lib.nfn_allreduce_mean(None, None, 1, None, None, None, None) == _lib.NFN_E_NULLPTR
+    assert native_lib.nfn_allreduce_mean(None, None, 1, None, None, None) == _lib.NFN_E_NULLPTR
     assert "allreduce" in _lib.last_error()
     assert native_lib.nfn_comm_destroy(None) == _lib.NFN_OK
 
