@@ -583,7 +583,7 @@ def main():
             metric = f"Chain bijector forward+fldj evals/sec (whole node), {args.config}"
         elif args.mode == "flows":
             kernel_name = (f"flow_fwd_ldj_kernel x {len(ft)} launches"
-                           + (" after split_blocks_kernel" if args.flow_params == "views" else ""))
+                           + (" after split_blocks_kernel" if getattr(launcher, "_split", None) is not None else ""))
             metric = f"flow-by-flow bijector forward+fldj chain evals/sec (whole node), {args.config}"
         elif args.mode == "dense":
             if S is None:

@@ -49,6 +49,54 @@ __global__ void __launch_bounds__(kMaxBlock)
 
 namespace {
 
+// The same single bijector for d > 1 with coalesced row traffic: a workgroup's 256 samples
+// stage their parameter rows (ps floats at t_rowstride) and their z rows (d floats at
+// z_bstride) into LDS at odd strides — whole-tile spans, coalesced — each lane evaluates
+// its sample from LDS, and z_out leaves through the same LDS region as one contiguous
+// (rows x d) run.  (One lane per row straight from global memory, the generic kernel
+// above, makes every wave instruction touch 64 rows' lines.)
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock)
+    flow_fwd_ldj_tile_kernel(int32_t flow_id, const float* __restrict__ z_in, int64_t z_bstride,
+                             const float* __restrict__ tk, int64_t t_rowstride, int64_t B, int32_t d, int32_t ps,
+                             float* __restrict__ z_out, float* __restrict__ ldj_out) {
+  extern __shared__ float lds[];
+  const int rows = blockDim.x;
+  const int tid = threadIdx.x;
+  const int SP = ps | 1, SZ = d | 1;
+  float* tp = lds;               // rows x SP parameters
+  float* tz = lds + rows * SP;   // rows x SZ inputs, then outputs
+  const int64_t b0 = (int64_t)blockIdx.x * rows;
+  const int nr = (int)min((int64_t)rows, B - b0);
+  const bool tb = t_rowstride == 0, zb = z_bstride == 0;
+  stage_rows(tp, tk + (tb ? 0 : b0 * t_rowstride), t_rowstride, tb ? 1 : nr, ps, SP, false);
+  stage_rows(tz, z_in + (zb ? 0 : b0 * z_bstride), z_bstride, zb ? 1 : nr, d, SZ, false);
+  __syncthreads();
+  const bool act = tid < nr;
+  float z[DM];
+  float ldj = 0.0f;
+  if (act) {
+    const float* zr = tz + (zb ? 0 : tid * SZ);
+#pragma unroll
+    for (int j = 0; j < DM; ++j) z[j] = (j < d) ? zr[j] : 0.0f;
+    ldj = flow_step<DM, FAST>(flow_id, z, tp + (tb ? 0 : tid * SP), d);
+  }
+  __syncthreads();  // every lane has read its z row (a broadcast row is shared) before any write
+  if (act) {
+    if (ldj_out) ldj_out[b0 + tid] = ldj;
+#pragma unroll
+    for (int j = 0; j < DM; ++j)
+      if (j < d) tz[tid * SZ + j] = z[j];
+  }
+  __syncthreads();
+  if (z_out) {
+    for (int i = tid; i < nr * d; i += rows) {
+      const int r = i / d, c = i - (i / d) * d;
+      z_out[b0 * d + i] = tz[r * SZ + c];
+    }
+  }
+}
+
 // The Bijector API's Chain (tfp Chain of the flows that InverseNormalizingFlowLayer.
 // _get_bijector builds, DistributionLayers.py:267-278): forward and
 // forward_log_det_jacobian in ONE launch instead of one or two per flow.  A tile of
@@ -128,6 +176,16 @@ template <int DM, bool FAST>
 void launch_f(int32_t flow_id, const float* z, int64_t zs, const float* tk, int64_t ts, int64_t B, int32_t d,
               float* z_out, float* ldj_out, hipStream_t s) {
   const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
+  if constexpr (DM > 1) {
+    // d > 1: LDS-staged rows (NFN_FLOW_VARIANT=0, diag A/B: the per-lane global reads)
+    if (env_int("NFN_FLOW_VARIANT", 1) != 0) {
+      const int ps = flow_id == NFN_FLOW_PLANAR ? 2 * d + 1 : (flow_id == NFN_FLOW_RADIAL ? d + 2 : 2 * d);
+      const size_t lds = (size_t)kMaxBlock * ((ps | 1) + (d | 1)) * sizeof(float);
+      auto kt = flow_fwd_ldj_tile_kernel<DM, FAST>;
+      kt<<<dim3((unsigned)nblk), dim3(kMaxBlock), lds, s>>>(flow_id, z, zs, tk, ts, B, d, ps, z_out, ldj_out);
+      return;
+    }
+  }
   // NFN_FLOW_VARIANT=0 (diag A/B): the generic bijector code for d = 1 too
   auto k = env_int("NFN_FLOW_VARIANT", 1) == 0 ? flow_fwd_ldj_kernel<DM, FAST, 0> : flow_fwd_ldj_kernel<DM, FAST, 1>;
   hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, flow_id, z, zs, tk, ts, B, d, z_out, ldj_out);

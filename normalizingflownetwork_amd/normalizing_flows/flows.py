@@ -39,13 +39,16 @@ class SplitBlocks:
     only when a flow is called on its own (the one-launch Chain reads the wide rows
     directly), and remade if ``base`` was modified in place since (torch version counter).
     Why: a single-flow launch over a view of the wide rows fetches each row's whole 128-B
-    lines for its few parameters (per-flow Bijector)."""
+    lines for its few parameters (per-flow Bijector).  Used only where that costs
+    more than the split's own pass (``ops.split_pays``: narrow blocks in wide rows)."""
 
     def __init__(self, base, widths):
         self.base = base
         self.widths = [int(w) for w in widths]
         self._blocks = None
         self._version = None
+        rs = int(base.stride(0)) if base.dim() == 2 else sum(self.widths)
+        self.pays = ops.split_pays(self.widths, rs)  # else the flows read their views directly
 
     def version(self):
         """The base tensor's in-place version counter, or None for a tensor that has none
@@ -88,7 +91,7 @@ class _ConditionedFlow(Bijector):
         if (self._split is not None and t.dim() == 2 and t.shape[0] > 1 and t.stride(0) != t.shape[1]
                 and not (torch.is_grad_enabled() and t.requires_grad)):
             group, k = self._split
-            if group.version() is not None:
+            if group.pays and group.version() is not None:
                 return group.blocks()[k]
         return t
 

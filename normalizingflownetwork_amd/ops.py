@@ -626,6 +626,20 @@ def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, w
     return z_out, ldj
 
 
+def split_pays(widths: Sequence[int], row_stride: int) -> bool:
+    """Whether the flows' single launches should read one-pass contiguous copies of their
+    blocks (``split_blocks``) rather than their strided views, by expected HBM bytes per
+    sample: a view launch fetches the whole 128-B lines its block touches (about
+    ``128 + 4 (w - 1)`` bytes for a block of w floats at a random offset), the split reads the
+    row once and writes and re-reads the blocks (``4 row_stride + 8 sum(w)``).  The split must
+    win by 30 % to pay for its own pass: C2's 3-float blocks of 32-float rows (368 vs 1360 B)
+    take it, C3's 10-17-float blocks of 140-float rows (1552 vs 1612 B) do not (measured:
+    1.43 vs 4.32 ms and 2.60 vs 2.02 ms, profiles/r03/r03s2_*, r03c3g_*)."""
+    strided = sum(128 + 4 * (int(w) - 1) for w in widths)
+    split = 4 * int(row_stride) + 8 * sum(int(w) for w in widths)
+    return split < 0.7 * strided
+
+
 def split_blocks(t: torch.Tensor, widths: Sequence[int]):
     """``[t[:, o_k:o_k + w_k].contiguous() for each block]`` in ONE pass over ``t``
     (``nfn_split_blocks_f32``): ``t`` (B, >= sum(widths)) device rows with unit column
@@ -767,10 +781,11 @@ class FlowsLauncher:
     previous flow's z, writing z and its own log|det J| (``ldj`` (K, B)).  ``z_out`` holds
     z_K after ``launch()``.  ``params`` says where the parameters come from:
 
-    * ``"views"`` (what ``normalizing_flows`` does for the flows of one layer's ``t``): each
-      ``launch()`` first makes the flows' blocks contiguous in ONE pass over ``t``
-      (``nfn_split_blocks_f32``, as TF's slices copy them), then runs the K launches on the
-      contiguous blocks;
+    * ``"views"`` (what ``normalizing_flows`` does for the flows of one layer's ``t``): when
+      ``split_pays`` (narrow blocks in wide rows, e.g. C2) each ``launch()`` first makes the
+      flows' blocks contiguous in ONE pass over ``t`` (``nfn_split_blocks_f32``, as TF's slices
+      copy them), then runs the K launches on the contiguous blocks; otherwise (C3) the
+      launches read their blocks from the rows (``mode`` becomes ``"strided"``);
     * ``"separate"``: the flows were built individually, each over its own contiguous
       (B, param_size) tensor (copied here, once, outside the timed launches);
     * ``"strided"``: each launch reads its block straight from the wide rows of ``t``
@@ -799,6 +814,8 @@ class FlowsLauncher:
         self._calls = []
         self._split = None
         self.params = []  # the flows' contiguous parameter tensors (kept alive here)
+        if self.mode == "views" and not split_pays([param_size(f, d) for f in flow_types], _row_stride(t) or P):
+            self.mode = "strided"  # the package's flows read such blocks straight from the rows
         if self.mode != "strided" and K:
             # blocks in row order: flow K-1 first (the layer's reversed layout)
             order = sorted(range(K), key=lambda k: offs[k])

@@ -5,6 +5,8 @@
       posterior agrees with the single-range one (NFN_POST_SPLIT=1)
   python tests/diag_modes.py grad_stream  -- NFN_DIAG build: the d = 1 straight-line
       backward (NFN_GRAD_WAVE1=1) equals the release's generic wave kernel bitwise
+  python tests/diag_modes.py flow_tile    -- NFN_DIAG build: the LDS-staged per-flow kernel (d > 1)
+      equals the per-lane global-read one bitwise (NFN_FLOW_VARIANT=0)
   python tests/diag_modes.py release      -- release build under ablation / tuning knobs in
       the environment: results are the oracle's (the knobs are compiled out)
 Prints one JSON line; exits non-zero on a mismatch."""
@@ -104,6 +106,43 @@ def grad_stream():
     return res
 
 
+def flow_tile():
+    """Per-flow bijector at d > 1: the LDS-staged kernel (default) against the per-lane
+    global-read kernel (NFN_FLOW_VARIANT=0) — the same flow_step on the same values, so z
+    and log|det J| must be bitwise equal; ragged batches, strided / broadcast rows."""
+    import torch
+
+    from normalizingflownetwork_amd import _lib
+
+    _lib.use_diagnostic_build()
+    from normalizingflownetwork_amd import ops
+
+    res = {"library": os.path.basename(_lib.LIB_PATH)}
+    n = 0
+    for d in (2, 3, 8, 16):
+        for ft in ("planar", "radial", "affine"):
+            ps = ops.param_size(ft, d)
+            for B, bz, bt in ((777, False, False), (256, False, False), (1000, True, False), (300, False, True)):
+                gen = torch.Generator(device="cuda").manual_seed(B + d)
+                wide = torch.randn((B, ps + 5), generator=gen, device="cuda")
+                tk = wide[:1, 2:2 + ps] if bt else wide[:, 2:2 + ps]
+                z = torch.randn((1 if bz else B, d), generator=gen, device="cuda")
+                outs = []
+                for v in ("1", "0"):
+                    os.environ["NFN_FLOW_VARIANT"] = v
+                    try:
+                        outs.append(ops.flow_forward_ldj(ft, z, tk, d))
+                    finally:
+                        os.environ.pop("NFN_FLOW_VARIANT")
+                (z1, l1), (z0, l0) = outs
+                for a, b, what in ((z1, z0, "z"), (l1, l0, "ldj")):
+                    same = (a == b) | (torch.isnan(a) & torch.isnan(b))
+                    assert bool(same.all()), f"{ft} d={d} B={B} bz={bz} bt={bt} {what}: {int((~same).sum())} differ"
+                n += 1
+    res["cases"] = n
+    return res
+
+
 def release():
     from normalizingflownetwork_amd import _lib, ops
 
@@ -127,4 +166,4 @@ def release():
 
 if __name__ == "__main__":
     which = sys.argv[1]
-    print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream}[which]()}), flush=True)
+    print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream, "flow_tile": flow_tile}[which]()}), flush=True)
