@@ -132,3 +132,14 @@ def test_noise_regularisation_values():
     m = NormalizingFlowNetwork(1, n_flows=1, noise_reg=("bogus", 3.0))
     with pytest.raises(AssertionError):
         m._assign_noise_regularisation(n_dims=2, n_datapoints=300)
+
+
+def test_split_pays_rule():
+    # ops.split_pays: the per-flow calls read one-pass copies of their blocks only where the
+    # expected bytes say so (C2: 10 blocks of 3 floats in 32-float rows; C3: affine + 4 planar
+    # + 4 radial at d = 8 in 140-float rows)
+    from normalizingflownetwork_amd import ops
+    assert ops.split_pays([3] * 10, 32)
+    assert not ops.split_pays([16] + [17] * 4 + [10] * 4, 140)
+    # a wide row holding one narrow block: the split would read the whole row for 12 B
+    assert not ops.split_pays([3], 1024)
