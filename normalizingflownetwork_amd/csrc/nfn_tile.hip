@@ -49,13 +49,42 @@ __global__ void __launch_bounds__(kMaxBlock)
 
 namespace {
 
+// Row staging for the per-flow tile kernel with eight loads in flight per lane before
+// their LDS writes (stage_rows' loop waits for each load in turn: at ps = 17 and d = 8
+// that is 25 dependent round trips per workgroup, and the kernel is latency-bound).
+__device__ __forceinline__ void stage_rows_x8(float* lds, const float* __restrict__ src, int64_t rs, int nr,
+                                              int P, int S) {
+  const int nth = blockDim.x, tid = threadIdx.x;
+  const int n = nr * P;
+  const int step_r = nth / P, step_c = nth - (nth / P) * P;
+  int r = tid / P, c = tid - (tid / P) * P;
+  for (int i0 = tid; i0 < n; i0 += 8 * nth) {
+    float v[8];
+    int o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      o[u] = r * S + c;
+      v[u] = (i0 + u * nth < n) ? src[(int64_t)r * rs + c] : 0.0f;
+      r += step_r;
+      c += step_c;
+      if (c >= P) {
+        c -= P;
+        r += 1;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u * nth < n) lds[o[u]] = v[u];
+  }
+}
+
 // The same single bijector for d > 1 with coalesced row traffic: a workgroup's 256 samples
 // stage their parameter rows (ps floats at t_rowstride) and their z rows (d floats at
 // z_bstride) into LDS at odd strides — whole-tile spans, coalesced — each lane evaluates
 // its sample from LDS, and z_out leaves through the same LDS region as one contiguous
 // (rows x d) run.  (One lane per row straight from global memory, the generic kernel
 // above, makes every wave instruction touch 64 rows' lines.)
-template <int DM, bool FAST>
+template <int DM, bool FAST, bool X8>
 __global__ void __launch_bounds__(kMaxBlock)
     flow_fwd_ldj_tile_kernel(int32_t flow_id, const float* __restrict__ z_in, int64_t z_bstride,
                              const float* __restrict__ tk, int64_t t_rowstride, int64_t B, int32_t d, int32_t ps,
@@ -69,8 +98,13 @@ __global__ void __launch_bounds__(kMaxBlock)
   const int64_t b0 = (int64_t)blockIdx.x * rows;
   const int nr = (int)min((int64_t)rows, B - b0);
   const bool tb = t_rowstride == 0, zb = z_bstride == 0;
-  stage_rows(tp, tk + (tb ? 0 : b0 * t_rowstride), t_rowstride, tb ? 1 : nr, ps, SP, false);
-  stage_rows(tz, z_in + (zb ? 0 : b0 * z_bstride), z_bstride, zb ? 1 : nr, d, SZ, false);
+  if constexpr (X8) {
+    stage_rows_x8(tp, tk + (tb ? 0 : b0 * t_rowstride), t_rowstride, tb ? 1 : nr, ps, SP);
+    stage_rows_x8(tz, z_in + (zb ? 0 : b0 * z_bstride), z_bstride, zb ? 1 : nr, d, SZ);
+  } else {
+    stage_rows(tp, tk + (tb ? 0 : b0 * t_rowstride), t_rowstride, tb ? 1 : nr, ps, SP, false);
+    stage_rows(tz, z_in + (zb ? 0 : b0 * z_bstride), z_bstride, zb ? 1 : nr, d, SZ, false);
+  }
   __syncthreads();
   const bool act = tid < nr;
   float z[DM];
@@ -177,11 +211,13 @@ void launch_f(int32_t flow_id, const float* z, int64_t zs, const float* tk, int6
               float* z_out, float* ldj_out, hipStream_t s) {
   const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
   if constexpr (DM > 1) {
-    // d > 1: LDS-staged rows (NFN_FLOW_VARIANT=0, diag A/B: the per-lane global reads)
+    // d > 1: LDS-staged rows (NFN_FLOW_VARIANT=0, diag A/B: the per-lane global reads;
+    // NFN_FLOW_STAGE=0: one load in flight per lane while staging)
     if (env_int("NFN_FLOW_VARIANT", 1) != 0) {
       const int ps = flow_id == NFN_FLOW_PLANAR ? 2 * d + 1 : (flow_id == NFN_FLOW_RADIAL ? d + 2 : 2 * d);
       const size_t lds = (size_t)kMaxBlock * ((ps | 1) + (d | 1)) * sizeof(float);
-      auto kt = flow_fwd_ldj_tile_kernel<DM, FAST>;
+      auto kt = env_int("NFN_FLOW_STAGE", 1) != 0 ? flow_fwd_ldj_tile_kernel<DM, FAST, true>
+                                                  : flow_fwd_ldj_tile_kernel<DM, FAST, false>;
       kt<<<dim3((unsigned)nblk), dim3(kMaxBlock), lds, s>>>(flow_id, z, zs, tk, ts, B, d, ps, z_out, ldj_out);
       return;
     }

@@ -634,7 +634,8 @@ def split_pays(widths: Sequence[int], row_stride: int) -> bool:
     row once and writes and re-reads the blocks (``4 row_stride + 8 sum(w)``).  The split must
     win by 30 % to pay for its own pass: C2's 3-float blocks of 32-float rows (368 vs 1360 B)
     take it, C3's 10-17-float blocks of 140-float rows (1552 vs 1612 B) do not (measured:
-    1.43 vs 4.32 ms and 2.60 vs 2.02 ms, profiles/r03/r03s2_*, r03c3g_*)."""
+    1.43 vs 4.32 ms and 2.60 vs 2.02 ms, profiles/r03/r03s2_*, r03c3g_*; C3 reading the
+    rows is 1.82 ms since, r03j_*)."""
     strided = sum(128 + 4 * (int(w) - 1) for w in widths)
     split = 4 * int(row_stride) + 8 * sum(int(w) for w in widths)
     return split < 0.7 * strided
