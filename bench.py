@@ -269,7 +269,7 @@ def main():
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only for tests)")
-    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad", "bijector", "flows"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "grad", "dense", "dense_grad", "bijector", "flows", "grid"],
                     help="forward = fused log_prob (the headline); grad = the fused backward of the "
                          "mean-NLL training step (d/dt, d/dy for a uniform upstream gradient); dense = the "
                          "output Dense layer (H -> P) fused into the chain, streaming h instead of t; "
@@ -277,6 +277,9 @@ def main():
                          "bijector = the Bijector API's Chain.forward + forward_log_det_jacobian over the "
                          "layer's flows in one launch (no base density); flows = the same Chain flow by flow, "
                          "one single-flow launch per flow (nfn_flow_fwd_ldj_f32)")
+    ap.add_argument("--grid", type=int, default=256,
+                    help="--mode grid: grid values G (each evaluated under every one of the B parameter rows; "
+                         "B defaults to 2^16, so G x B = 2^24 evals as at C2)")
     ap.add_argument("--hidden", type=int, default=16, help="--mode dense / dense_grad: hidden width H")
     ap.add_argument("--event-every", type=int, default=1,
                     help="time the dominant kernel with HIP events on every E-th timed step (default: every "
@@ -336,6 +339,16 @@ def main():
             launcher = ops.DenseGradLauncher(y, h, Wd, bd, ft, d, True, g_out=g_up)
         else:
             launcher = (ops.DenseLauncher if S is None else ops.PosteriorDenseLauncher)(y, h, Wd, bd, ft, d, True)
+    elif args.mode == "grid":
+        # the density grid of flow_plotting.plot_model: G y values x B parameter rows
+        assert S is None, "--mode grid covers the plain chain configs (C2, C3)"
+        if not args.batch:
+            B = 1 << 16
+        G = args.grid
+        yg = (torch.linspace(-4.0, 4.0, G, device=dev).reshape(G, 1).repeat(1, d).contiguous() if d == 1 else
+              torch.randn((G, d), generator=gen, device=dev))
+        t = torch.randn((B, P), generator=gen, device=dev)
+        launcher = ops.GridLauncher(yg, t, ft, d, True)
     elif args.mode in ("bijector", "flows"):
         assert S is None, "--mode bijector / flows cover the plain chain configs (C2, C3)"
         t = torch.randn((B, P), generator=gen, device=dev)
@@ -363,7 +376,7 @@ def main():
         and getattr(launcher, "fused_sum", False)
     works = [None, None]
     nstep = [0]
-    evals_per_step = B * (1 if S is None else S)
+    evals_per_step = B * (1 if S is None else S) * (args.grid if args.mode == "grid" else 1)
     native = None
     if dist_on and args.allreduce == "native":
         from normalizingflownetwork_amd.parallel import NativeComm
@@ -382,7 +395,7 @@ def main():
         launcher.launch(sh)
         if ev1 is not None:
             ev1.record(stream)
-        if grad_mode or args.mode in ("bijector", "flows"):  # per-sample outputs stay on their rank
+        if grad_mode or args.mode in ("bijector", "flows", "grid"):  # per-sample outputs stay on their rank
             return
         if direct:
             works[i] = dist.all_reduce(reds[i], async_op=True)
@@ -525,7 +538,7 @@ def main():
         if dense_mode:
             del t_buf, plain
     nonfinite = None
-    if grad_mode or args.mode in ("bijector", "flows"):
+    if grad_mode or args.mode in ("bijector", "flows", "grid"):
         mean_ll = None
     elif native is not None:
         mean_ll = float(native.mean.item())
@@ -552,6 +565,9 @@ def main():
         elif args.mode == "flows":
             # per flow: z in, its block of t, z and its ldj out (the K launches of one step)
             bytes_launch = launcher.bytes_per_launch
+        elif args.mode == "grid":
+            # the B parameter rows and G grid values once, the (G, B) log-densities out
+            bytes_launch = float(B) * 4 * P + float(args.grid) * 4 * d + float(args.grid) * B * 4
         elif args.mode == "dense_grad":
             # h, y, upstream g in; dh, dy out; W, b read and dW, db written once per launch
             bytes_launch = float(B) * (8 * H + 8 * d + 4) + 2 * (4.0 * H * P + 4.0 * P)
@@ -559,12 +575,12 @@ def main():
             bytes_launch = algorithmic_bytes_per_launch(d, P, B, S)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = load_traffic(args.config + {"grad": "_grad", "dense": "_dense", "dense_grad": "_dense_grad",
-                                                           "bijector": "_bijector",
+                                                           "bijector": "_bijector", "grid": "_grid",
                                                            "flows": "_flows" if args.flow_params == "views" else "_flows_" + args.flow_params
                                                            }.get(args.mode, ""), B)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline("bijector" if args.mode == "flows" else args.mode, args.config, H=H,
+            cpu = cpu_baseline({"flows": "bijector", "grid": "forward"}.get(args.mode, args.mode), args.config, H=H,
                                seconds=args.cpu_seconds)
         wl = {
             "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
@@ -585,6 +601,9 @@ def main():
             kernel_name = (f"flow_fwd_ldj_kernel x {len(ft)} launches"
                            + (" after split_blocks_kernel" if getattr(launcher, "_split", None) is not None else ""))
             metric = f"flow-by-flow bijector forward+fldj chain evals/sec (whole node), {args.config}"
+        elif args.mode == "grid":
+            kernel_name = "chain_grid_kernel"
+            metric = f"density-grid log_prob evals/sec (whole node), {args.config} (G={args.grid} grid values x B rows)"
         elif args.mode == "dense":
             if S is None:
                 kernel_name = "chain_dense1_kernel" if d == 1 else "chain_dense_kernel"
@@ -628,8 +647,12 @@ def main():
                 "allreduce": None if (world == 1 or grad_mode) else args.allreduce,
                 "mode": args.mode,
                 **({"flow_params": args.flow_params} if args.mode == "flows" else {}),
+                **({"grid": args.grid} if args.mode == "grid" else {}),
             },
             "roofline": {
+                **({"note": "compute-bound: the parameter rows are read once for all G grid values, so the "
+                            "HBM fraction is small by construction; DESIGN.md compares the evals/s with the "
+                            "C2 forward's compute-only rate"} if args.mode == "grid" else {}),
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

@@ -775,6 +775,32 @@ class BijectorLauncher:
             _lib.check(rc, "nfn_chain_fwd_ldj_f32")
 
 
+class GridLauncher:
+    """Pre-bound density grid (``nfn_chain_logprob_grid_f32``) for the benchmark: the
+    ``log_prob`` of each of G grid values under each of B parameter rows, (G, B) out — the
+    evaluation ``flow_plotting.plot_model`` makes (``evaluation/visualization/flow_plotting.py:33-53``)."""
+
+    def __init__(self, y_grid: torch.Tensor, t: torch.Tensor, flow_types: Sequence[str], n_dims: int,
+                 trainable_base: bool):
+        self.lib = _lib.load()
+        d = int(n_dims)
+        P = total_param_size(flow_types, d, trainable_base)
+        assert y_grid.dim() == 2 and y_grid.shape[1] == d and y_grid.stride(1) == 1
+        assert t.dim() == 2 and t.shape[1] == P and t.stride(1) == 1
+        self.G, self.B = int(y_grid.shape[0]), int(t.shape[0])
+        self.y_grid, self.t = y_grid, t
+        self.out = torch.empty((self.G, self.B), dtype=torch.float32, device=t.device)
+        self._ids, self._k = flow_ids(flow_types)
+        self._args = (_ptr(y_grid), int(y_grid.stride(0)) if self.G > 1 else 0, self.G, _ptr(t), _row_stride(t),
+                      self.B, d, ctypes.cast(self._ids, ctypes.c_void_p), self._k, int(bool(trainable_base)),
+                      None, None, _ptr(self.out), self.B)
+
+    def launch(self, stream: Optional[int] = None) -> None:
+        rc = self.lib.nfn_chain_logprob_grid_f32(*self._args, stream if stream is not None else _stream())
+        if rc != 0:
+            _lib.check(rc, "nfn_chain_logprob_grid_f32")
+
+
 class FlowsLauncher:
     """Pre-bound flow-by-flow Bijector path for the benchmark: the Chain's K flows as K
     single-flow launches (``nfn_flow_fwd_ldj_f32``, PlanarFlow.py:68-80 / RadialFlow.py:50-70 /

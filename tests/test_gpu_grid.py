@@ -74,3 +74,28 @@ def test_grid_equals_per_row_prob(gpu):
     y = (np.linspace(3, -3, 40).reshape(40, 1) - m.y_mean) / m.y_std
     loop = np.stack([dist.prob(y[i].astype(np.float32)).cpu().numpy() for i in range(40)]) / np.sum(m.y_std)
     np.testing.assert_allclose(heat, loop, rtol=1e-5, atol=1e-30)  # exp of log_prob < -87 is denormal
+
+
+def test_grid_launcher_equals_op(gpu):
+    """bench.py --mode grid's pre-bound launcher computes what ops.chain_log_prob_grid does,
+    at the bench's shape (G = 256 grid values x 2^16 C2 parameter rows), and matches the
+    oracle on a random subset of (g, b) pairs."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d = ("planar", "radial") * 5, 1
+    P = O.total_param_size(ft, d, True)
+    G, B = 256, 1 << 16
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    t = torch.randn((B, P), generator=gen, device="cuda")
+    yg = torch.linspace(-4.0, 4.0, G, device="cuda").reshape(G, 1).contiguous()
+    lz = ops.GridLauncher(yg, t, ft, d, True)
+    lz.launch()
+    ref = ops.chain_log_prob_grid(yg, t, ft, d, True)
+    torch.cuda.synchronize()
+    assert torch.equal(lz.out, ref)
+    rng = np.random.default_rng(0)
+    gi, bi = rng.integers(0, G, 2048), rng.integers(0, B, 2048)
+    tn, ygn = t.cpu().numpy(), yg.cpu().numpy()
+    r64 = O.log_pdf(ygn[gi], tn[bi], ft, d, True, None, None, np.float64)
+    r32 = O.log_pdf(ygn[gi], tn[bi], ft, d, True, None, None, np.float32)
+    check_forward(lz.out.cpu().numpy()[gi, bi], r64, r32, "grid bench shape G=256 B=2^16 (2048 pairs)", kind="grid")
