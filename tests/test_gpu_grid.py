@@ -99,3 +99,28 @@ def test_grid_launcher_equals_op(gpu):
     r64 = O.log_pdf(ygn[gi], tn[bi], ft, d, True, None, None, np.float64)
     r32 = O.log_pdf(ygn[gi], tn[bi], ft, d, True, None, None, np.float32)
     check_forward(lz.out.cpu().numpy()[gi, bi], r64, r32, "grid bench shape G=256 B=2^16 (2048 pairs)", kind="grid")
+
+
+@pytest.mark.parametrize("ft", [("planar", "radial") * 5, ("affine", "radial", "planar"), ("radial",) * 3])
+def test_grid_d1_equals_fused_log_prob_bitwise(gpu, ft):
+    """At d = 1 (fast math) the grid forms each flow's parameter-only terms once per row
+    and runs only the z-dependent part per grid value: the same expressions as the fused
+    log_prob kernels, so every (g, b) equals log_prob(y_g | t_b) of ops.chain_log_prob
+    bit for bit (normalised y included)."""
+    from normalizingflownetwork_amd import ops
+
+    prev = ops.set_math_mode("fast")
+    try:
+        d = 1
+        P = O.total_param_size(ft, d, True)
+        rng = np.random.default_rng(len(ft))
+        B, G = 1000, 7
+        t = torch.from_numpy(rng.standard_normal((B, P)).astype(np.float32)).cuda()
+        yg = torch.from_numpy((rng.standard_normal((G, 1)) * 2).astype(np.float32)).cuda()
+        for ym, ys in ((None, None), (np.array([0.3], np.float32), np.array([1.7], np.float32))):
+            grid = ops.chain_log_prob_grid(yg, t, ft, d, True, ym, ys)
+            for g in range(G):
+                lp, _ = ops.chain_log_prob(yg[g:g + 1].expand(B, 1).contiguous(), t, ft, d, True, ym, ys)
+                assert torch.equal(grid[g], lp), (ft, g, ym is not None)
+    finally:
+        ops.set_math_mode(prev)
