@@ -39,7 +39,10 @@ __global__ void __launch_bounds__(1024) reduce_f64_kernel(const double* __restri
 // costs no HBM bytes) the tile's whole span [row0 * rs, (row0 + R - 1) * rs + W) is read as
 // 16-byte buffer loads, every lane active, from the 16-byte-aligned address at or below its
 // first float (`mis` floats lower; the descriptor is bounded at the last valid float, so
-// nothing outside t is read); otherwise row by row (one row's W dwords per wave
+// nothing past the tile is read; below it, the first tile reads the 0-3 floats between that
+// aligned address and t — inside t's 16-byte granule, so inside any allocation whose base is
+// 16-byte aligned, as every HIP and torch allocation is, but outside t itself: a host-side
+// checker that tracks t's exact span would flag them); otherwise row by row (one row's W dwords per wave
 // instruction).  The tile goes to LDS, then each block is written as its own contiguous
 // (rows x w) run, lanes over consecutive floats (row = e / w by a float reciprocal: e <
 // 2^18, so the quotient never rounds across an integer).  R * (span of a row) <= 16384

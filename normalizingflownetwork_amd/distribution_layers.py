@@ -19,7 +19,7 @@ import torch
 
 from . import ops
 from .normalizing_flows import FLOWS, Chain, Invert
-from .normalizing_flows.flows import SplitBlocks
+from .normalizing_flows.flows import SplitBlocks, snapshot_rows
 
 
 class TensorShape(tuple):
@@ -124,10 +124,22 @@ class FlowDistribution:
         self._trainable = bool(trainable_base_dist)
         self._t = t
         self.distribution = InverseNormalizingFlowLayer._get_base_dist(t, n_dims, trainable_base_dist)
-        flow_t = _cols(t, 2 * n_dims, _shape(t)[-1]) if trainable_base_dist else t
-        # Builds the Chain eagerly so a wrong width raises AssertionError at
-        # construction, as in the reference (DistributionLayers.py:272).
-        self.bijector = Invert(InverseNormalizingFlowLayer._get_bijector(flow_t, self._flow_types, n_dims))
+        # A wrong width raises AssertionError at construction, as in the reference
+        # (DistributionLayers.py:272); the Chain itself (and the parameter snapshot its flows
+        # own) is built on first use of ``bijector``: log_prob never needs it.
+        flow_w = _shape(t)[-1] - (2 * n_dims if trainable_base_dist else 0)
+        assert sum(FLOWS[f].get_param_size(n_dims) for f in self._flow_types) == flow_w
+        self._bijector = None
+
+    @property
+    def bijector(self):
+        """``Invert(Chain(flows))`` over a snapshot of ``t``'s flow columns taken on first
+        access (``_get_bijector``)."""
+        if self._bijector is None:
+            d = self._n_dims
+            flow_t = _cols(self._t, 2 * d, _shape(self._t)[-1]) if self._trainable else self._t
+            self._bijector = Invert(InverseNormalizingFlowLayer._get_bijector(flow_t, self._flow_types, d))
+        return self._bijector
 
     @property
     def event_shape(self):
@@ -253,18 +265,21 @@ class InverseNormalizingFlowLayer:
     @staticmethod
     def _get_bijector(t, flow_types, n_dims):
         """Chain of flows; blocks are split in REVERSED ``flow_types`` order and
-        ``bijectors[0]`` is the last flow type (``DistributionLayers.py:267-278``)."""
+        ``bijectors[0]`` is the last flow type (``DistributionLayers.py:267-278``).  As TF's
+        slices are copies, the flows own a snapshot of ``t`` taken here (one device pass,
+        ``flows.snapshot_rows``): later writes to ``t`` do not reach them."""
         flow_types = list(reversed(list(flow_types)))
         param_sizes = [FLOWS[flow_type].get_param_size(n_dims) for flow_type in flow_types]
         assert sum(param_sizes) == _shape(t)[-1]
+        t = snapshot_rows(t)
         chain = []
         begin = 0
         for size, flow_type in zip(param_sizes, flow_types):
             chain.append(FLOWS[flow_type](_cols(t, begin, begin + size), n_dims))
             begin += size
         if isinstance(t, torch.Tensor) and t.dim() == 2 and t.stride(-1) == 1 and len(chain) > 1:
-            # the flows' own launches read contiguous copies of their blocks, made in one
-            # pass on the first such call (TF's slices are copies; normalizing_flows.SplitBlocks)
+            # the flows' own launches read contiguous copies of their blocks of the snapshot,
+            # made in one pass on the first such call (normalizing_flows.SplitBlocks)
             group = SplitBlocks(t, param_sizes)
             for k, f in enumerate(chain):
                 f._split = (group, k)

@@ -31,16 +31,41 @@ def _width(t) -> int:
     return int(shape[-1])
 
 
+def snapshot_rows(t):
+    """A private copy of the (B, W) parameter tensor ``t`` for the flows ``_get_bijector``
+    builds: TF's ``t[:, o:o+size]`` slices there (``DistributionLayers.py:267-278``) are copies
+    of an immutable tensor, so a Chain keeps evaluating the parameters it was built from
+    whatever later happens to ``t`` — including writes torch cannot see (HIP-graph replays
+    into ``t``, raw-pointer / DLPack producers).  ONE pass on the device.  The copy's rows
+    keep the 16-byte phase the one-launch Chain kernel wants: ``(-W) mod 4`` lead columns
+    (never read) put the row start on a float4 boundary, as the layer's base columns do in
+    the wide ``t`` (C2: 2 + 30 = 32 floats).  A broadcast row (stride 0) stays one row.
+    Numpy / list inputs pass through (each flow moves its own slice: already a copy)."""
+    if not isinstance(t, torch.Tensor) or t.dim() != 2:
+        return t
+    t = t.detach()
+    B, W = int(t.shape[0]), int(t.shape[1])
+    if B > 1 and t.stride(0) == 0:
+        return t[:1].clone().expand(B, W)
+    lead = (-W) % 4
+    buf = torch.empty((B, W + lead), dtype=t.dtype, device=t.device)
+    buf[:, lead:].copy_(t)
+    return buf[:, lead:]
+
+
 class SplitBlocks:
-    """The contiguous copies of consecutive column blocks of one parameter tensor, made in
-    ONE pass (``ops.split_blocks`` -> ``nfn_split_blocks_f32``) on first use and shared by the
-    flows that hold views of those blocks.  TF's ``t[:, o:o+size]`` slices in
-    ``_get_bijector`` (``DistributionLayers.py:267-278``) ARE such copies; here they are made
-    only when a flow is called on its own (the one-launch Chain reads the wide rows
-    directly), and remade if ``base`` was modified in place since (torch version counter).
+    """The contiguous copies of consecutive column blocks of the flows' private parameter
+    snapshot (:func:`snapshot_rows`), made in ONE pass (``ops.split_blocks`` ->
+    ``nfn_split_blocks_f32``) on the first single-flow call and shared by the flows that
+    hold views of those blocks (the one-launch Chain reads the snapshot's rows directly).
     Why: a single-flow launch over a view of the wide rows fetches each row's whole 128-B
     lines for its few parameters (per-flow Bijector).  Used only where that costs
-    more than the split's own pass (``ops.split_pays``: narrow blocks in wide rows)."""
+    more than the split's own pass (``ops.split_pays``: narrow blocks in wide rows) and only
+    over real rows (a broadcast stride-0 row is already read once per line).
+    The snapshot belongs to the flows, so the copies can only go stale through a write into
+    a flow's own ``params``: torch in-place ops on them bump the version counter checked
+    here; a raw-pointer writer into ``params`` must call :meth:`release`.  :meth:`release`
+    also frees the copies' memory (B x sum(widths) floats) when the flows are done."""
 
     def __init__(self, base, widths):
         self.base = base
@@ -48,7 +73,13 @@ class SplitBlocks:
         self._blocks = None
         self._version = None
         rs = int(base.stride(0)) if base.dim() == 2 else sum(self.widths)
-        self.pays = ops.split_pays(self.widths, rs)  # else the flows read their views directly
+        # else the flows read their views directly
+        self.pays = rs >= sum(self.widths) and ops.split_pays(self.widths, rs)
+
+    def release(self):
+        """Drop the copies (remade on the next single-flow call)."""
+        self._blocks = None
+        self._version = None
 
     def version(self):
         """The base tensor's in-place version counter, or None for a tensor that has none

@@ -74,20 +74,31 @@ _ws_lock = threading.Lock()
 # (device, stream) workspaces kept at once; the least recently used is dropped beyond
 # this (pooled / side streams come and go: fit's capture stream, the bench's ring).
 WORKSPACE_CACHE_ENTRIES = 8
+# Workspaces a captured HIP graph may hold the address of: handed out while their stream
+# was capturing.  Kept alive for the life of the process (graphs do not tell when they die);
+# a graph's replays write partials and the ticket there, so the block must never go back
+# to the allocator.
+_graph_workspaces: list = []
 
 
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
     """The workspace of the current (device, stream): calls are ordered on their stream,
     so calls in flight on different streams never share partials, the posterior's split
     region or the finishing ticket.  No initialisation is needed (ABI 200: the ticket
-    carries a per-call epoch).  Dropping an entry is safe: its memory returns
-    to the caching allocator's pool of the SAME stream, so a later allocation that reuses
-    it is ordered after the calls that used it."""
-    key = (device.index, int(torch.cuda.current_stream(device).cuda_stream))
+    carries a per-call epoch).  Dropping (or outgrowing) an entry that no graph captured
+    is safe: its memory returns to the caching allocator's pool of the SAME stream, so a
+    later allocation that reuses it is ordered after the calls that used it.  An entry
+    used during a capture is pinned instead (``_graph_workspaces``): the graph keeps its
+    address, and eager warm-up calls on the capture stream commonly allocate it first."""
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, int(stream.cuda_stream))
+    capturing = torch.cuda.is_current_stream_capturing()
     with _ws_lock:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < n_doubles:
             ws = torch.empty(max(2, n_doubles), dtype=torch.float64, device=device)
+        if capturing and not any(p is ws for p in _graph_workspaces):
+            _graph_workspaces.append(ws)
         _workspaces[key] = ws
         _workspaces.move_to_end(key)
         while len(_workspaces) > WORKSPACE_CACHE_ENTRIES:

@@ -143,3 +143,50 @@ def test_split_pays_rule():
     assert not ops.split_pays([16] + [17] * 4 + [10] * 4, 140)
     # a wide row holding one narrow block: the split would read the whole row for 12 B
     assert not ops.split_pays([3], 1024)
+
+
+def test_get_bijector_snapshots_t():
+    """TF's slices in _get_bijector are copies (DistributionLayers.py:267-278): the flows own
+    a snapshot of t taken when the Chain is built, so a later write to t — in place, through
+    a raw pointer or a graph replay — does not reach them.  The snapshot keeps t's values,
+    puts each row start on a 16-byte boundary (C2: 2 lead + 30 columns) and keeps a
+    broadcast (stride-0) row a single row."""
+    from normalizingflownetwork_amd.normalizing_flows.flows import snapshot_rows
+
+    ft = ("planar", "radial") * 5
+    t = torch.randn(64, 32)
+    chain = InverseNormalizingFlowLayer._get_bijector(t[:, 2:], ft, 1)
+    before = [f._t.clone() for f in chain.bijectors]
+    t.mul_(3.0)
+    for f, b in zip(chain.bijectors, before):
+        assert torch.equal(f._t, b)
+    snap = chain.bijectors[0]._t
+    assert snap.stride(0) == 32 and snap.storage_offset() == 2
+    s = snapshot_rows(t[:, 1:])  # W = 31: 1 lead column
+    assert torch.equal(s, t[:, 1:]) and s.stride(0) == 32 and s.storage_offset() == 1
+    row = torch.randn(1, 30).expand(1000, 30)
+    s = snapshot_rows(row)
+    assert s.stride(0) == 0 and torch.equal(s, row) and s.data_ptr() != row.data_ptr()
+
+
+def test_split_group_skips_broadcast_rows():
+    """A stride-0 (broadcast) parameter row is read once per cache line by the flows'
+    own launches already: no split (nfn_split_blocks_f32 needs real rows)."""
+    ft = ("planar", "radial") * 5
+    chain = InverseNormalizingFlowLayer._get_bijector(torch.randn(1, 30).expand(4096, 30), ft, 1)
+    assert chain.bijectors[0]._split[0].pays is False
+    chain = InverseNormalizingFlowLayer._get_bijector(torch.randn(4096, 32)[:, 2:], ft, 1)
+    assert chain.bijectors[0]._split[0].pays is True
+
+
+def test_distribution_builds_its_bijector_on_first_use():
+    """FlowDistribution checks the width at construction (AssertionError, as the reference)
+    but builds the Chain — and the flows' parameter snapshot — only when ``bijector`` is
+    first read: log_prob never pays for the copy."""
+    layer = InverseNormalizingFlowLayer(("planar", "radial"), 1, True)
+    dist = layer(torch.zeros(8, 8))
+    assert dist._bijector is None
+    b = dist.bijector
+    assert b is dist.bijector and len(b.bijector.bijectors) == 2
+    with pytest.raises(AssertionError):
+        layer(torch.zeros(8, 9))

@@ -394,3 +394,43 @@ def test_graph_replay_repeats_epoch(kind, gpu):
         assert float(osum[0].item()) == pytest.approx(float(out.double().sum().item()), rel=1e-12), r
         assert float(osum[1].item()) == 0.0
         assert int(ws[1].item()) == 0, "the ticket is left at zero"
+
+
+def test_graph_workspace_survives_cache_eviction(gpu):
+    """ops._workspace hands a stream its cached workspace; an entry used while the stream
+    captures a graph is pinned, so pushing more than WORKSPACE_CACHE_ENTRIES other streams
+    through the cache (which evicts its least recently used entries) cannot return the
+    graph's workspace to the allocator: replays after the eviction still sum correctly
+    while other tensors are allocated and written on the capture stream's pool."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d, B = ("planar", "radial") * 5, 1, 100_000
+    gen = torch.Generator(device="cuda").manual_seed(21)
+    y = torch.randn((B, 1), generator=gen, device="cuda")
+    t = torch.randn((B, 32), generator=gen, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        _, s_eager = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)  # warm-up
+    torch.cuda.synchronize()
+    ref = float(s_eager[0].item())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        _, s_graph = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
+    (key,) = [k for k in ops._workspaces if k[1] == int(side.cuda_stream)]
+    ws = ops._workspaces[key]
+    assert any(p is ws for p in ops._graph_workspaces)
+    streams = [torch.cuda.Stream() for _ in range(ops.WORKSPACE_CACHE_ENTRIES + 2)]
+    for st in streams:
+        with torch.cuda.stream(st):
+            ops.chain_log_prob(y[:1000], t[:1000], ft, d, True, want_values=False, want_sum=True)
+    torch.cuda.synchronize()
+    assert key not in ops._workspaces  # evicted from the cache, still alive for the graph
+    with torch.cuda.stream(side):
+        junk = [torch.full((ws.numel(),), 7.0, dtype=torch.float64, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert float(s_graph[0].item()) == pytest.approx(ref, rel=1e-12)
+    assert all(float(j[0].item()) == 7.0 for j in junk)
