@@ -75,6 +75,10 @@ def record_parity(what, got, ref64, ref32, err, bound, kind="forward", sens32=No
     small = fin & (np.abs(ref64) < 1.0) & (ref64 != 0.0)
     widened = fin & (err > base)
     floor_only = small & (err > 1e-5 * np.abs(ref64)) & (err <= base)
+    # beyond both the 1e-5 base and the single-run gate WIDEN_CAP x |ref32 - ref64|: admitted
+    # only by the perturbed runs' fp32 sensitivity (tests/parity.py)
+    with np.errstate(invalid="ignore"):
+        by_pert = widened & (err > WIDEN_CAP * dev32) & (err <= bound)
     w = int(np.argmax(np.where(fin, err / np.maximum(bound, 1e-300), -1.0))) if err.size else 0
     PARITY.append({
         "check": what,
@@ -88,6 +92,9 @@ def record_parity(what, got, ref64, ref32, err, bound, kind="forward", sens32=No
         "n_small_ref": int(small.sum()),
         "n_floor_only": int(floor_only.sum()),
         "n_widened": int(widened.sum()),
+        "n_pass_only_by_perturbation": int(by_pert.sum()),
+        "max_err_over_base_unwidened": float((err[fin & ~widened] / base[fin & ~widened]).max())
+        if (fin & ~widened).any() else None,
         "widened_max_err_over_dev32": float((err[widened] / np.maximum(dev32[widened], 1e-300)).max())
         if widened.any() else None,
         "widened_max_err_over_base": float((err[widened] / base[widened]).max()) if widened.any() else None,
