@@ -465,6 +465,17 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
     }
     a.lds_stride = S;
   }
+#ifdef NFN_DIAG
+  // diagnostic A/B (NFN_GRAD_WAVE2=1; measured and not adopted, DESIGN.md "C2 backward"):
+  // d = 1, fast math, P = 8, 16 or 32, two samples per lane over 128-row wave tiles
+  const size_t slot2 = (size_t)(128 * S + a.prog.K * 128) * sizeof(float);
+  if (wave_ok && use_fast_math() && d == 1 && Q <= 8 && slot2 * 2 <= (size_t)80 * 1024 &&
+      env_int("NFN_GRAD_WAVE2", 0) == 1) {
+    a.ntiles = (B + 127) / 128;
+    int64_t grid = 0;
+    if (launch_grad_wave2(Q, ga, s, &grid)) return check_hip("chain_grad_wave2_kernel launch");
+  }
+#endif
   if (wave_ok) {
     a.ntiles = (B + 63) / 64;
     // two waves per workgroup measured fastest on C2 (finer LDS allocation granules

@@ -254,21 +254,28 @@ __device__ __forceinline__ float softplus_alpha(float x) {
   }
 }
 
-// tanh with RELATIVE accuracy (a few ulp) everywhere.  1 - 2 / (1 + e^{2a}) has an
-// absolute error of ~1e-7, i.e. a large relative one as a -> 0; a planar step multiplies
-// tanh by u_hat, which reaches ~1 / |w| when w -> 0 (u_hat ~ m / w), so the absolute
-// error became a z error of ~1e-7 / |w| (C2 full batch: log_prob off by up to 2e-4 on
-// 2e-5 of the samples, tests/test_gpu_fullbatch.py).  Below |a| = 0.3 the Taylor
-// polynomial to a^9 (truncation < 5e-8 relative); above it the exp form (< 4e-7).
+// tanh with RELATIVE accuracy everywhere (<= 1.7 ulp, 0.27 on average; tools/kernel_emu.py
+// with correctly rounded v_exp / v_rcp).  An absolute error of ~1e-7 is a large relative one
+// as a -> 0; a planar step multiplies tanh by u_hat, which reaches ~1 / |w| when w -> 0
+// (u_hat ~ m / w), so the absolute error became a z error of ~1e-7 / |w| (C2 full batch:
+// log_prob off by up to 2e-4 on 2e-5 of the samples, tests/test_gpu_fullbatch.py).
+// Below |a| = 0.55 an odd minimax polynomial (tanh(a) / a - 1 as five terms in a^2, fitted
+// for relative error on [0, 0.55]: <= 0.75 ulp); above it 1 - 2 / (1 + e^{2|a|}) with the
+// sign copied back (<= 2.2 ulp at 0.55, 1.3 past 1; e^{2|a|} -> inf saturates to 1).  The
+// round-3 form (Taylor to a^9 below 0.3, 1 - 2 / (1 + e^{2a}) at signed a) reached 5.2 ulp on
+// the negative side, where 2 / (1 + e^{2a}) > 1 has twice the ulp; this one costs two VALU
+// more per evaluation (measured: C2 +1.8 %, C5 +1.3 %, profiles/r04/r04c_*).
 __device__ __forceinline__ float tanh_fast(float a) {
-  const float E = __builtin_amdgcn_exp2f(a * (2.0f * kLog2e));
-  const float te = 1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f));  // saturates to +-1 cleanly
+  const float x = fabsf(a);
+  const float E = __builtin_amdgcn_exp2f(x * (2.0f * kLog2e));
+  const float te = copysignf(1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f)), a);
   const float a2 = a * a;
-  float p = fmaf(a2, 62.0f / 2835.0f, -17.0f / 315.0f);
-  p = fmaf(a2, p, 2.0f / 15.0f);
-  p = fmaf(a2, p, -1.0f / 3.0f);
+  float p = fmaf(a2, -0.0062827035f, 0.021077914f);
+  p = fmaf(a2, p, -0.053853896f);
+  p = fmaf(a2, p, 0.13332602f);
+  p = fmaf(a2, p, -0.3333332f);
   const float tp = fmaf(a * a2, p, a);
-  return fabsf(a) < 0.3f ? tp : te;
+  return x < 0.55f ? tp : te;
 }
 
 template <bool FAST>

@@ -583,4 +583,5 @@ bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_
               : launch_wave_t<false>(dm, nv, ga, lds_block, waves_per_block, s, grid);
 }
 
+
 }  // namespace nfn

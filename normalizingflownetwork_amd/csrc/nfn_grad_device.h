@@ -11,6 +11,14 @@
 
 #include "nfn_device.h"
 
+// Contraction of a * b + c into an fma only within one source expression (as written),
+// never by the backend across expressions: the adjoints are then evaluated the same way
+// in every kernel that inlines them (one or two samples per lane, any chain form), so the
+// backward kernels agree bitwise.  (The build default, fast-honor-pragmas, lets the backend
+// fuse across statements, and its choices follow the surrounding code.)  Restored at the
+// end of this header.  Measured cost on the C2 backward: none (profiles/r04/r04c_*).
+#pragma clang fp contract(on)
+
 namespace nfn {
 
 template <bool FAST>
@@ -385,6 +393,135 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
   return lp;
 }
 
+
+// The base density's adjoint (grad1_packed's, row-major tile): writes d/d(loc, scale
+// param) into row[0..1] and returns d log_prob / d z_K.
+__device__ __forceinline__ float base1_bwd(float z, float* row, bool trainable, float gl) {
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[1], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    row[0] = gz;
+    row[1] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+    return -gz;
+  }
+  return -gl * z;
+}
+
+// grad1_packed for TWO samples per lane (the rows ra, rb of one wave tile, flow inputs at
+// zha / zhb) under ONE walk of the program: the flow dispatch, the block offsets and the
+// parameter-read schedule are shared, and the two samples' arithmetic forms two
+// independent dependency chains for the scheduler to interleave — the streaming backward
+// (chain_grad_wave2_kernel) then hides the chain's latency with half the resident waves.
+// Per sample it is exactly grad1_packed's arithmetic in grad1_packed's order (bitwise).
+template <class Mid = NoMid>
+__device__ __forceinline__ void grad1_packed2(float& za, float& zb, float* ra, float* rb, float* zha, float* zhb,
+                                              int zs, uint32_t types, int K, int P, bool trainable, float gla,
+                                              float glb, bool want_lp, float& adja, float& adjb, float& lpa,
+                                              float& lpb, const Mid& mid = Mid{}) {
+  float l2a = 0.0f, l2b = 0.0f;
+  int id = (int)(types & 3u);
+  int off = max(P - size1(id), 0);
+  float pa[3], pb[3];
+  if (K > 0) {
+    read3c(pa, ra, off);
+    read3c(pb, rb, off);
+  }
+#pragma unroll 1
+  for (int k = 0; k < 16; ++k) {
+    if (k < K) {
+      const int idn = (int)((types >> (2 * (k + 1) & 31)) & 3u);
+      const int offn = max(off - size1(idn), 0);
+      float na[3], nb[3];
+      read3c(na, ra, offn);
+      read3c(nb, rb, offn);
+      zha[k * zs] = za;
+      zhb[k * zs] = zb;
+      if (id == NFN_FLOW_PLANAR) {
+        if (want_lp) {
+          l2a += __builtin_amdgcn_logf(fabsf(planar1_fast(za, pa[0], pa[1], pa[2])));
+          l2b += __builtin_amdgcn_logf(fabsf(planar1_fast(zb, pb[0], pb[1], pb[2])));
+        } else {
+          planar1_z(za, pa[0], pa[1], pa[2]);
+          planar1_z(zb, pb[0], pb[1], pb[2]);
+        }
+      } else if (id == NFN_FLOW_RADIAL) {
+        if (want_lp) {
+          l2a += __builtin_amdgcn_logf(fabsf(radial1_fast(za, pa[0], pa[1], pa[2])));
+          l2b += __builtin_amdgcn_logf(fabsf(radial1_fast(zb, pb[0], pb[1], pb[2])));
+        } else {
+          radial1_z(za, pa[0], pa[1], pa[2]);
+          radial1_z(zb, pb[0], pb[1], pb[2]);
+        }
+      } else {
+        if (want_lp) {
+          l2a += __builtin_amdgcn_logf(fabsf(affine1_fast(za, pa[0], pa[1])));
+          l2b += __builtin_amdgcn_logf(fabsf(affine1_fast(zb, pb[0], pb[1])));
+        } else {
+          za = fmaf(za, 1.0f + pa[1], pa[0]);
+          zb = fmaf(zb, 1.0f + pb[1], pb[0]);
+        }
+      }
+      id = idn;
+      off = offn;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pa[i] = na[i];
+        pb[i] = nb[i];
+      }
+    }
+  }
+  lpa = want_lp ? base1_fast<1>(za, ra, trainable) + l2a * kLn2 : 0.0f;
+  lpb = want_lp ? base1_fast<1>(zb, rb, trainable) + l2b * kLn2 : 0.0f;
+  mid();
+  float a1a = base1_bwd(za, ra, trainable, gla);
+  float a1b = base1_bwd(zb, rb, trainable, glb);
+  int ob = trainable ? 2 : 0;
+  int ib = (int)((types >> (2 * (K - 1) & 31)) & 3u);
+  float qa[3] = {0.0f, 0.0f, 0.0f}, qb[3] = {0.0f, 0.0f, 0.0f};
+  float zba = 0.0f, zbb = 0.0f;
+  if (K > 0) {
+    read3c(qa, ra, ob);
+    read3c(qb, rb, ob);
+    zba = zha[(K - 1) * zs];
+    zbb = zhb[(K - 1) * zs];
+  }
+#pragma unroll 1
+  for (int k = 15; k >= 0; --k) {
+    if (k < K) {
+      const int ip = (int)((types >> (2 * (k - 1) & 31)) & 3u);
+      const int op = min(ob + size1(ib), P - 1);  // k = 0: a harmless in-slot read
+      float ppa[3], ppb[3];
+      read3c(ppa, ra, op);
+      read3c(ppb, rb, op);
+      const float zpa = zha[max(k - 1, 0) * zs];
+      const float zpb = zhb[max(k - 1, 0) * zs];
+      if (ib == NFN_FLOW_PLANAR) {
+        planar1_bwd(zba, a1a, qa[0], qa[1], qa[2], ra + ob, gla);
+        planar1_bwd(zbb, a1b, qb[0], qb[1], qb[2], rb + ob, glb);
+      } else if (ib == NFN_FLOW_RADIAL) {
+        radial1_bwd(zba, a1a, qa[0], qa[1], qa[2], ra + ob, gla);
+        radial1_bwd(zbb, a1b, qb[0], qb[1], qb[2], rb + ob, glb);
+      } else {
+        affine1_bwd(zba, a1a, qa[0], qa[1], ra + ob, gla);
+        affine1_bwd(zbb, a1b, qb[0], qb[1], rb + ob, glb);
+      }
+      ib = ip;
+      ob = op;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        qa[i] = ppa[i];
+        qb[i] = ppb[i];
+      }
+      zba = zpa;
+      zbb = zpb;
+    }
+  }
+  adja = a1a;
+  adjb = a1b;
+}
 
 // grad1_packed with two flows per dispatch in both passes (chain1_fast_pairs): each of
 // the nine (type, type) bodies is straight-line code.  Same arithmetic in the same
@@ -802,3 +939,5 @@ __device__ __forceinline__ float grad_sample(float (&z)[DM], float* row, float* 
 }
 
 }  // namespace nfn
+
+#pragma clang fp contract(fast)

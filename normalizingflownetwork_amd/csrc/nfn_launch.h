@@ -114,6 +114,11 @@ void launch_grad(bool fast, int dm, const GradArgs& ga, dim3 grid, size_t lds, h
 // wave-owned persistent form; false if (dm, nv) has no instance
 bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_block, int waves_per_block,
                       hipStream_t s, int64_t* grid);
+#ifdef NFN_DIAG
+// nfn_grad.hip (diag A/B): d = 1 fast-math backward with two samples per lane (128-row
+// wave tiles), P = 4Q with Q in {2, 4, 8}; false for other Q
+bool launch_grad_wave2(int Q, const GradArgs& ga, hipStream_t s, int64_t* grid);
+#endif
 // nfn_grad_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance
 bool launch_grad_group_fast(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s,

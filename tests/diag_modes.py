@@ -68,10 +68,12 @@ def strategies():
 
 
 def grad_stream():
-    """d = 1 backward: the straight-line buffer pipeline (chain_grad_wave1_kernel, diag
+    """d = 1 backward: the two-samples-per-lane kernel (chain_grad_wave2_kernel, diag
+    NFN_GRAD_WAVE2=1), the straight-line buffer pipeline (chain_grad_wave1_kernel, diag
     NFN_GRAD_WAVE1=1, in one or two prefetch pieces) and the producer / consumer workgroup
-    (chain_grad_pc_kernel, NFN_GRAD_PC=1) against the release's generic wave kernel: the same per-sample math, so log_prob, d/dt and d/dy must be bitwise equal
-    (NaN where both are)."""
+    (chain_grad_pc_kernel, NFN_GRAD_PC=1) against the release's wave kernel
+    (chain_grad_wave_kernel): the same per-sample math, so log_prob, d/dt and d/dy must be
+    bitwise equal (NaN where both are)."""
     import torch
 
     from normalizingflownetwork_amd import _lib
@@ -90,15 +92,17 @@ def grad_stream():
         g = torch.randn((B,), generator=gen, device="cuda")
         ym, ys = (np.float32([norm[0]]), np.float32([norm[1]])) if norm else (None, None)
         outs = {}
-        for v, split, pc in (("0", "1", "0"), ("1", "1", "0"), ("1", "2", "0"), ("0", "1", "1")):
+        for v, split, pc, w2 in (("0", "1", "0", "0"), ("1", "1", "0", "0"), ("1", "2", "0", "0"),
+                                 ("0", "1", "1", "0"), ("0", "1", "0", "1")):
             os.environ["NFN_GRAD_WAVE1"], os.environ["NFN_GRAD_SPLIT"], os.environ["NFN_GRAD_PC"] = v, split, pc
+            os.environ["NFN_GRAD_WAVE2"] = w2
             try:
-                outs[v + split + pc] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
+                outs[v + split + pc + w2] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
             finally:
-                for k in ("NFN_GRAD_WAVE1", "NFN_GRAD_SPLIT", "NFN_GRAD_PC"):
+                for k in ("NFN_GRAD_WAVE1", "NFN_GRAD_SPLIT", "NFN_GRAD_PC", "NFN_GRAD_WAVE2"):
                     os.environ.pop(k)
-        outs["01"] = outs["010"]
-        for alt in ("110", "120", "011"):
+        outs["01"] = outs["0100"]
+        for alt in ("1100", "1200", "0110", "0101"):
             for a, b, what in zip(outs[alt], outs["01"], ("log_prob", "grad_t", "grad_y")):
                 same = (a == b) | (torch.isnan(a) & torch.isnan(b))
                 assert bool(same.all()), f"{ft} B={B} {alt} {what}: {int((~same).sum())} values differ"
@@ -149,12 +153,14 @@ def release():
     knobs = {k: v for k, v in os.environ.items() if k.startswith("NFN_")}
     assert knobs.get("NFN_ABLATE_FLOWS") == "1", "run with the knobs set"
     res = {"library": os.path.basename(_lib.LIB_PATH), "knobs": knobs}
+    from parity import check_forward, fp32_sensitivity
+
     for name in ("c2_pr5_d1", "c3_apr_d8", "stress_pr5_d1"):
         g = load_golden(name)
         lp, _ = ops.chain_log_prob(g["y"], g["t"], g["flow_types"], g["d"], bool(g["trainable"]))
-        err = np.abs(lp.cpu().numpy().astype(np.float64) - g["ref64"])
-        ok = err <= O.tolerance_bound(g["ref64"], g["ref32"])
-        assert ok.all(), f"{name}: {int((~ok).sum())} samples off under the knobs"
+        # the suite's forward gate (tests/parity.py), as in test_gpu_parity's fixture checks
+        check_forward(lp.cpu().numpy(), g["ref64"], g["ref32"], f"{name} under the knobs",
+                      sensitivity=fp32_sensitivity(g["y"], g["t"], g["flow_types"], g["d"], bool(g["trainable"])))
         res[name] = "oracle parity"
     gp = load_golden("posterior_s8_pr5_d1")
     out, _ = ops.posterior_lse(gp["y"], gp["t"], gp["flow_types"], 1, True, gp["y_mean"], gp["y_std"])

@@ -383,9 +383,14 @@ def test_chain_bijector_one_launch(name, d, gpu):
     chain = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d)
     fz = chain._fused()
     assert fz is not None
-    # the fused view starts at the row start left of the first block (the base columns), so
-    # the layer's rows stream whole (d = 1: the wave1 pipeline; d = 8: the lane-group one)
-    assert fz[1].data_ptr() == t.data_ptr() and min(fz[2]) == 2 * d
+    # the flows own a snapshot of t's flow columns (TF's slices are copies), whose rows start
+    # (-W) mod 4 lead columns left of the first block on a 16-byte boundary; the fused view
+    # starts at that row start, so the rows stream whole (d = 1: the wave1 pipeline; d = 8:
+    # the lane-group one)
+    W = t.shape[1] - 2 * d
+    lead = (-W) % 4
+    assert fz[1].data_ptr() == chain.bijectors[0].params.data_ptr() - 4 * lead and min(fz[2]) == lead
+    assert fz[1].stride(0) == W + lead and fz[1].data_ptr() % 16 == 0
     launches = []
     real = ops.chain_forward_ldj
 
@@ -402,12 +407,12 @@ def test_chain_bijector_one_launch(name, d, gpu):
     assert len(launches) == 3
     # flow by flow through the single-flow kernel (a Chain of copies: no shared storage);
     # bitwise the one-launch result where both run the generic per-flow math (the tile
-    # kernel: d = 3, and d = 16 whose 134-float rows are not float4 rows); d = 1 (wave1) and
-    # d = 8 (lane groups) run the fast-math chain forms — all are held to the oracle below
+    # kernel: d = 3); d = 1 (wave1) and d = 8, 16 (lane groups over the snapshot's float4
+    # rows) run the fast-math chain forms — all are held to the oracle below
     steps = Chain([type(b)(b.params.clone(), d) for b in chain.bijectors])
     assert steps._fused() is None
     z1, ldj1 = steps.forward_and_log_det_jacobian(y)
-    if d in (3, 16):
+    if d == 3:
         assert torch.equal(z, z1) and torch.equal(ldj, ldj1)
     # against the oracle's flows applied in the same order (fp64 truth, fp32 op-by-op mirror
     # for the conditioning term), through the forward tolerance

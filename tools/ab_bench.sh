@@ -18,7 +18,8 @@ for r in $(seq 1 ${REPS:-3}); do
         > "$OUT/${cfg}_${v}_$r.json" 2> "$OUT/${cfg}_${v}_$r.err"
       rc=$?
       echo "$cfg $v $r rc=$rc $(python -c "import json,sys; d=json.loads([l for l in open('$OUT/${cfg}_${v}_$r.json') if l.startswith('{')][0]); print(round(d['roofline']['kernel_ms'],4), round(d['ms_per_step'],4))" 2>/dev/null)"
-      [ $rc -ne 0 ] && exit $rc
+      if [ $rc -ne 0 ]; then exit $rc; fi
     done
   done
 done
+exit 0

@@ -581,6 +581,19 @@ def main():
             run_grad(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                            {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}], rounds=4)
         return
+    if which[0] == "grad2":  # d = 1 backward: two samples per lane (wave2, 128-row tiles, diag) vs one (wave)
+        W2 = {"NFN_GRAD_WAVE2": 1}
+        for cfg in ("C2", "C1"):
+            run_grad(cfg, [{"name": "wave", "env": {}}, {"name": "wave2", "env": dict(W2)},
+                           {"name": "wave_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                           {"name": "wave2_memory_only", "env": dict(W2, NFN_ABLATE_FLOWS=1)},
+                           {"name": "wave_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
+                           {"name": "wave2_compute_only", "env": dict(W2, NFN_ABLATE_LOADS=1)},
+                           {"name": "wave2_wg2", "env": dict(W2, NFN_WG_PER_CU=2)},
+                           {"name": "wave2_wg2_memory_only", "env": dict(W2, NFN_WG_PER_CU=2, NFN_ABLATE_FLOWS=1)},
+                           {"name": "wave2_noprio", "env": dict(W2, NFN_PRIO=0)},
+                           {"name": "wave_b", "env": {}}, {"name": "wave2_b", "env": dict(W2)}], rounds=4)
+        return
     if which[0] == "gradw1":  # d = 1 backward: straight-line buffer pipeline vs the generic wave kernel
         for cfg in ("C2", "C1"):
             G = {"NFN_GRAD_WAVE1": 0}

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Launch one config's forward kernel a few times under a diagnostic-build knob (for
-rocprofv3 --pmc passes over a single variant: run it as the program after `--`).
+"""Launch one config's forward kernel (or, with --grad, its fused backward) a few times
+under a diagnostic-build knob (for rocprofv3 --pmc passes over a single variant: run it as
+the program after `--`).
 
-  python3 tools/run_variant.py C2 NFN_WAVE1_DMA=1 [--launches 5]"""
+  python3 tools/run_variant.py C2 NFN_WAVE1_DMA=1 [--launches 5]
+  python3 tools/run_variant.py C2 NFN_GRAD_WAVE2=1 --grad"""
 
 import os
 import sys
@@ -17,6 +19,7 @@ def main():
     ap.add_argument("cfg")
     ap.add_argument("knobs", nargs="*", help="NAME=VALUE diagnostic-build knobs")
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--grad", action="store_true", help="the fused backward (GradLauncher) instead")
     a = ap.parse_args()
     cfg, knobs, n = a.cfg, dict(k.split("=", 1) for k in a.knobs), a.launches
     os.environ.update(knobs)  # read by the diag library at each launch
@@ -33,6 +36,15 @@ def main():
     gen = torch.Generator(device="cuda").manual_seed(1)
     y = torch.randn((B, d), generator=gen, device="cuda")
     t = torch.randn((B, P) if S is None else (S, B, P), generator=gen, device="cuda")
+    if a.grad:
+        g = torch.full((B,), -1.0 / B, device="cuda")
+        L = ops.GradLauncher(y, t, ft, d, True, g_out=g)
+        for _ in range(n):
+            L.launch(int(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        print({"cfg": cfg, "knobs": knobs, "launches": n, "grad": True,
+               "grad_t_abs_sum": float(L.grad_t.double().abs().sum().item())})
+        return
     L = ops.ChainLauncher(y, t, ft, d, True, draws=S)
     for _ in range(n):
         L.launch()
