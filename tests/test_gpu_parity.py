@@ -330,7 +330,9 @@ def test_maximum_sizes(d, K, math_mode):
     r32 = O.posterior_lse(y, np.stack([t, t[::-1]]), ft, d, True, dtype=np.float32)
     assert_within(post.cpu().numpy(), r64, r32, f"max posterior d={d} K={K}")
     _, gt, gy = ops.chain_log_prob_grad(torch.from_numpy(y).cuda(), torch.from_numpy(t).cuda(), ft, d, True)
-    gt64, gy64, dev_t, dev_y = G.fp32_spread(y, t, ft, d, True, n_perturbed=1)
+    # the gradient gate's standard spread (the fp32 autodiff at the inputs and at three 1-ulp
+    # perturbations, nfn_grad_oracle.fp32_spread's default, as in every other gradient check)
+    gt64, gy64, dev_t, dev_y = G.fp32_spread(y, t, ft, d, True)
     for got, ref, dev in ((gt.cpu().numpy(), gt64, dev_t), (gy.cpu().numpy(), gy64, dev_y)):
         ok = np.isfinite(ref)
         ratio = np.abs(got - ref)[ok] / G.grad_tolerance(ref, dev)[ok]
