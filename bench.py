@@ -13,7 +13,7 @@ and per-workgroup fp64 partial sums) + the partials reduce + (N > 1) the
 all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
 resident in HBM before the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5|C3P]
                   [--mode forward|grad|dense|dense_grad|bijector|flows [--flow-params views|separate|strided]]
   N > 1: either under a launcher (python -m torch.distributed.run --nproc-per-node N ...
   bench.py --gpus N), or plain `python bench.py --gpus N`, which starts that launcher as a
@@ -46,6 +46,9 @@ CONFIGS = {
     "C2": (C2_FLOWS, 1, 1 << 24, None),
     "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22, None),
     "C5": (C2_FLOWS, 1, 1 << 17, 64),
+    # C5's posterior over C3's flow stack at y_dim 3 (P = 60: inside the fused Dense path's
+    # P <= 64; C3's own d = 8, P = 140 is not) — the d >= 2 posterior Dense kernel's line
+    "C3P": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 3, 1 << 17, 64),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -586,6 +589,7 @@ def main():
             "C2": "C2: y_dim=1, (planar,radial)x5 chain, batch 2^24 per GPU" + (" (C4 form: RCCL mean-NLL all-reduce)" if world > 1 else ""),
             "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
             "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
+            "C3P": "C3P: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=3, affine+planar x4+radial x4 (P = 60)",
         }[args.config]
         if args.mode == "grad":
             kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group1_kernel"
@@ -609,11 +613,12 @@ def main():
                 kernel_name = "chain_dense1_kernel" if d == 1 else "chain_dense_kernel"
                 metric = f"Dense(H={H})->log_prob evals/sec (whole node), {args.config}"
             else:
-                kernel_name = "posterior_dense1_kernel" if d == 1 else "posterior_dense_kernel"
+                kernel_name = ("posterior_dense1_kernel" if d == 1 else
+                               "posterior_densep_kernel" if (H <= 16 and args.math == "fast") else "posterior_dense_kernel")
                 metric = f"DenseVariational(H={H})->posterior (draw, sample) evals/sec (whole node), {args.config}"
         else:
             kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel",
-                           "C5": "posterior_wave1_kernel"}[args.config]
+                           "C5": "posterior_wave1_kernel", "C3P": "chain_persistent_kernel (posterior)"}[args.config]
             metric = ("log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"
                       if args.config == "C2" else f"log_prob evals/sec (whole node), {args.config}")
         line = {

@@ -523,6 +523,198 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense_kernel(DenseArgs da
   }
 }
 
+// The posterior with the output DenseVariational layer fused for d >= 2 (fast math, H in
+// {4, 8, 16}, P <= 64): posterior_dense1_kernel's memory pipeline around the generic chain.
+// A wave walks (tile, draw) units — its 64-sample tile through all S draws; the NEXT
+// unit's h tile (QH float4 per lane), W_s B-fragments (QH x NN per lane) and bias are
+// buffer-prefetched through descriptors bounded at B (counted waits, no per-lane
+// branches) while the current unit runs t_s = h_s W_s + b_s on the matrix cores
+// (v_mfma_f32_16x16x4_f32, exact fp32) into the wave's row-major t tile, the chain
+// (eval_chain, one sample per lane) and the online logsumexp; the tile's y rows are
+// prefetched with its first draw and its score leaves once, after its last draw.
+// posterior_dense_kernel (synchronous loads, W_s fragments from L2) stays the precise-math
+// and wide-H form.
+template <int DM, int QH>
+__global__ void __launch_bounds__(kMaxBlock) posterior_densep_kernel(DenseArgs da) {
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  __shared__ double red[2 * kMaxBlock / 64];
+  constexpr int RSTEP = 64 / QH;
+  constexpr int kNT = 2;
+  constexpr int NNMAX = 4;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int SH = da.h_lds_stride;
+  const int S = a.lds_stride;
+  const int P = a.P;
+  const int d = a.d;
+  const int NN = (P + 15) >> 4;
+  const int ND = a.S;  // draws
+  float* hl = lds + wid * (64 * SH + 64 * S);
+  float* tl = hl + 64 * SH;
+  const int r0 = lane / QH, c4 = lane % QH;
+  const int l0 = r0 * SH + 4 * c4;
+  const int am = lane & 15, ak = lane >> 4;
+  const int64_t hs = da.h_rowstride;
+  const int64_t ntiles = a.ntiles;
+  const int64_t u0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const bool norm = a.y_mean != nullptr;
+  float corr = 0.0f;
+  if (norm) {
+    for (int j = 0; j < d; ++j) corr += f_log<true>(a.y_std[j]);
+  }
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int hoff = (r0 * (int)hs + 4 * c4) * 4;
+  const int kstep = RSTEP * (int)hs * 4;
+  int woff[QH][NNMAX];  // this lane's B-fragment offsets in W_s (bytes); columns >= P read row 0 and are zeroed
+  bool wcol[NNMAX];
+#pragma unroll
+  for (int nt = 0; nt < NNMAX; ++nt) {
+    wcol[nt] = 16 * nt + am < P;
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks) woff[ks][nt] = wcol[nt] ? ((4 * ks + ak) * P + 16 * nt + am) * 4 : 0;
+  }
+  float4 buf[QH];
+  float ybuf[DM];
+  float wbuf[QH][NNMAX], bbuf[NNMAX];
+  auto issue = [&](int64_t tile, int sd) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    if (sd == 0) {  // the tile's y rows, with its first draw
+      const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + d) * 4 : 0);
+#pragma unroll
+      for (int j = 0; j < DM; ++j)
+        ybuf[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff + 4 * min(j, d - 1), 0, 0));
+    }
+    const auto rh = tile_rsrc(da.h + sd * da.h_drawstride + b0c * hs, nr > 0 ? ((nr - 1) * hs + 4 * QH) * 4 : 0);
+#pragma unroll
+    for (int k = 0; k < QH; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, k * kstep, kNT));
+    const auto rw = tile_rsrc(da.W + sd * da.w_drawstride, nr > 0 ? (int64_t)4 * QH * P * 4 : 0);
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < NNMAX; ++nt)
+        wbuf[ks][nt] = nt < NN ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, woff[ks][nt], 0, 0))
+                               : 0.0f;
+    const auto rb = tile_rsrc(da.bias ? da.bias + sd * da.b_drawstride : da.W, (da.bias && nr > 0) ? P * 4 : 0);
+#pragma unroll
+    for (int nt = 0; nt < NNMAX; ++nt)
+      bbuf[nt] = nt < NN ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (16 * nt + am) * 4, 0, 0))
+                         : 0.0f;
+  };
+  double acc_sum = 0.0;
+  int nfc = 0;  // non-finite log_prob values
+  __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
+  float pend_v = 0.0f;
+  auto flush = [&]() {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  };
+  issue(u0, 0);
+  flush();  // empty: every path into the loop ends [loads][store]
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    float z0[DM];
+    float m = -INFINITY, lacc = 0.0f;
+    for (int sd = 0; sd < ND; ++sd) {
+#pragma unroll
+      for (int k = 0; k < QH; ++k) {
+        float* dst = hl + l0 + k * RSTEP * SH;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
+      float wv[QH][NNMAX], bv[NNMAX];
+#pragma unroll
+      for (int nt = 0; nt < NNMAX; ++nt) {
+        bv[nt] = bbuf[nt];
+#pragma unroll
+        for (int ks = 0; ks < QH; ++ks) wv[ks][nt] = wcol[nt] ? wbuf[ks][nt] : 0.0f;
+      }
+      if (sd == 0) {
+#pragma unroll
+        for (int j = 0; j < DM; ++j) {
+          z0[j] = j < d ? ybuf[j] : 0.0f;
+          if (norm && j < d) z0[j] = f_div<true>(z0[j] - a.y_mean[j], a.y_std[j]);
+        }
+      }
+      wave_lds_sync();
+      const bool last = sd + 1 == ND;
+      issue(last ? tile + ustep : tile, last ? 0 : sd + 1);
+      flush();
+      pend_r = tile_rsrc(a.out, 0);  // later draws of this tile store nothing
+      float av[4][QH];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < QH; ++ks) av[mt][ks] = hl[(16 * mt + am) * SH + 4 * ks + ak];
+#pragma unroll
+      for (int nt = 0; nt < NNMAX; ++nt) {
+        if (nt < NN) {
+          f32x4v acc[4];
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+              acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][ks], wv[ks][nt], acc[mt], 0, 0, 0);
+          const int n = 16 * nt + am;
+          if (n < P) {
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) tl[(16 * mt + 4 * ak + i) * S + n] = acc[mt][i] + bv[nt];
+            }
+          }
+        }
+      }
+      wave_lds_sync();
+      float z[DM];
+#pragma unroll
+      for (int j = 0; j < DM; ++j) z[j] = z0[j];
+      const float lp = eval_chain<DM, true>(z, tl + lane * S, a) - corr;
+      lse_push<true>(m, lacc, lp);
+      wave_lds_sync();  // this unit's LDS reads done before the next unit's writes
+    }
+    const float res = lse_finish<true>(m, lacc, ND);
+    if (lane < nr) {
+      acc_sum += (double)res;
+      nfc += nonfinite1(res);
+    }
+    pend_v = res;
+    pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+  }
+  flush();
+  if (a.partials) {
+    write_partial(a.partials, acc_sum, nfc, red, a.out_sum, a.epoch, a.pair_base);
+  }
+}
+
+template <int DM, int QH>
+void launch_pdp(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
+  auto kfn = posterior_densep_kernel<DM, QH>;
+  const size_t lds = (size_t)(4 * (64 * da.h_lds_stride + 64 * da.c.lds_stride) + 16) * sizeof(float);
+  const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
+  *grid_out = std::max<int64_t>(1, grid);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+}
+
+template <int DM>
+bool launch_pdp_h(const DenseArgs& da, hipStream_t s, int64_t* g) {
+  switch (da.H >> 2) {
+    case 1: launch_pdp<DM, 1>(da, s, g); return true;
+    case 2: launch_pdp<DM, 2>(da, s, g); return true;
+    case 4: launch_pdp<DM, 4>(da, s, g); return true;
+  }
+  return false;
+}
+
 template <int QH>
 void launch_pd1(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
@@ -563,6 +755,19 @@ bool launch_pd_dm(int dm, const DenseArgs& da, hipStream_t s, int64_t* g) {
         case 4: launch_pd1<4>(da, s, g); return true;
         case 8: launch_pd1<8>(da, s, g); return true;
       }
+    }
+  }
+  if constexpr (FAST) {
+    // d >= 2, H <= 16: the prefetching pipeline (NFN_DENSEP=0, diag: the synchronous kernel)
+    if (dm >= 2 && a.d >= 2 && da.H <= 16 && env_int("NFN_DENSEP", 1) != 0 && da.h_rowstride * 256 < ((int64_t)1 << 31) &&
+        a.y_bstride * 256 < ((int64_t)1 << 31)) {
+      bool ok = false;
+      switch (dm) {
+        case 2: ok = launch_pdp_h<2>(da, s, g); break;
+        case 4: ok = launch_pdp_h<4>(da, s, g); break;
+        case 8: ok = launch_pdp_h<8>(da, s, g); break;
+      }
+      if (ok) return true;
     }
   }
   switch (dm) {

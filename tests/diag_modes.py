@@ -7,6 +7,8 @@
       backward (NFN_GRAD_WAVE1=1) equals the release's generic wave kernel bitwise
   python tests/diag_modes.py flow_tile    -- NFN_DIAG build: the LDS-staged per-flow kernel (d > 1)
       equals the per-lane global-read one bitwise (NFN_FLOW_VARIANT=0)
+  python tests/diag_modes.py densep       -- NFN_DIAG build: the prefetching d >= 2 posterior Dense
+      kernel equals the synchronous one bitwise (NFN_DENSEP=0)
   python tests/diag_modes.py release      -- release build under ablation / tuning knobs in
       the environment: results are the oracle's (the knobs are compiled out)
 Prints one JSON line; exits non-zero on a mismatch."""
@@ -110,6 +112,46 @@ def grad_stream():
     return res
 
 
+def densep():
+    """Posterior with the output DenseVariational layer fused, d >= 2, fast math: the
+    prefetching pipeline (posterior_densep_kernel, default) against the synchronous kernel
+    (posterior_dense_kernel, NFN_DENSEP=0) — the same MFMA accumulation order, chain and
+    logsumexp, so the scores must be bitwise equal; per-draw and shared h, y normalisation,
+    no bias, ragged batches."""
+    import torch
+
+    from normalizingflownetwork_amd import _lib
+
+    _lib.use_diagnostic_build()
+    from normalizingflownetwork_amd import ops
+
+    res = {"library": os.path.basename(_lib.LIB_PATH)}
+    c3 = ("affine",) + ("planar",) * 4 + ("radial",) * 4
+    cases = [(c3, 3, 16, 4099, 5, False, True, False), (("radial", "planar"), 2, 4, 65, 3, True, True, True),
+             (("planar", "radial", "affine"), 8, 8, 300, 2, False, False, True), (c3, 3, 16, 1, 64, True, True, False)]
+    for ft, d, H, B, S, shared, bias, normed in cases:
+        P = ops.total_param_size(ft, d, True)
+        gen = torch.Generator(device="cuda").manual_seed(B + d)
+        y = torch.randn((B, d), generator=gen, device="cuda")
+        h = torch.randn((B, H) if shared else (S, B, H), generator=gen, device="cuda")
+        W = torch.randn((S, H, P), generator=gen, device="cuda") / float(np.sqrt(H))
+        b = 0.1 * torch.randn((S, P), generator=gen, device="cuda") if bias else None
+        ym, ys = (np.full(d, 0.3, np.float32), np.full(d, 1.7, np.float32)) if normed else (None, None)
+        outs = []
+        for v in ("1", "0"):
+            os.environ["NFN_DENSEP"] = v
+            try:
+                outs.append(ops.posterior_lse_dense(y, h, W, b, ft, d, True, ym, ys, want_sum=True))
+            finally:
+                os.environ.pop("NFN_DENSEP")
+        (o1, s1), (o0, s0) = outs
+        same = (o1 == o0) | (torch.isnan(o1) & torch.isnan(o0))
+        assert bool(same.all()), f"d={d} H={H} B={B} S={S}: {int((~same).sum())} scores differ"
+        assert torch.equal(s1, s0), f"d={d} H={H} B={B} S={S}: sums differ"
+        res[f"d{d}_H{H}_B{B}_S{S}"] = "bitwise"
+    return res
+
+
 def flow_tile():
     """Per-flow bijector at d > 1: the LDS-staged kernel (default) against the per-lane
     global-read kernel (NFN_FLOW_VARIANT=0) — the same flow_step on the same values, so z
@@ -172,4 +214,5 @@ def release():
 
 if __name__ == "__main__":
     which = sys.argv[1]
-    print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream, "flow_tile": flow_tile}[which]()}), flush=True)
+    print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream, "flow_tile": flow_tile,
+                             "densep": densep}[which]()}), flush=True)

@@ -91,6 +91,11 @@ def _post_case(ft, d, H, B, S, seed, shared_h=False, bias=True):
     (("affine", "planar", "radial"), 3, 8, 300, 4, False),  # generic posterior kernel (d > 1)
     (("planar", "affine"), 8, 16, 129, 3, True),
     (("planar", "radial") * 2, 1, 32, 65, 1, False),     # S = 1
+    # d >= 2, H <= 16, fast math: the prefetching posterior_densep_kernel (C3's flow stack at
+    # d = 3, P = 60; a ragged last tile; h shared; H = 4)
+    (("affine",) + ("planar",) * 4 + ("radial",) * 4, 3, 16, 777, 6, False),
+    (("radial", "planar"), 2, 4, 65, 3, True),
+    (("planar", "radial", "affine"), 4, 16, 1, 2, False),
 ])
 def test_posterior_dense_matches_oracle(math_mode, ft, d, H, B, S, shared):
     """Bayesian posterior score with the output DenseVariational layer fused
@@ -213,10 +218,10 @@ def test_dense_grad_full_size_against_oracle(gpu):
       planar w -> 0): the 0.5 % of rows with entries above 1e6 carry essentially all of
       sum |dt|, so they set both the sums and their bounds.  dW and db are therefore ALSO
       checked on a second launch whose upstream gradient is zero on every row with an oracle
-      gradient entry above 100 in magnitude (about 10 % of the rows; their dt, hence their
-      share of dW and db, is then exactly 0): the remaining rows' sums against the oracle's
-      over the same rows, where the bound is a few % of the sums instead of orders of
-      magnitude above them.
+      gradient entry above 100 in magnitude or a first-launch dh entry above 25 (about 10 %
+      of the rows; their dt, hence their share of dW and db, is then exactly 0): the
+      remaining rows' sums against the oracle's over the same rows, where the bound is a
+      few % of the sums instead of orders of magnitude above them.
     The upstream gradient is N(0, 1) per row (unit scale, so the 2e-5 floor is not slack)."""
     from concurrent.futures import ThreadPoolExecutor
 
@@ -246,6 +251,8 @@ def test_dense_grad_full_size_against_oracle(gpu):
                 "dense grad dh C2 full batch (4096 random rows)", kind="dense_grad")
     check_grad(gyn[idx], gy64, dev_y, "dense grad dy C2 full batch (4096 random rows)")
 
+    ghmax = np.abs(ghn).max(axis=1)
+
     def chunk(lo):
         hi = min(B, lo + (1 << 20))
         hc, gc = hn[lo:hi].astype(np.float64), gn[lo:hi].astype(np.float64)[:, None]
@@ -267,7 +274,11 @@ def test_dense_grad_full_size_against_oracle(gpu):
                 _, g32, _ = A.chain_grad(yk, tk, ft, d, True, dtype=np.float32)
                 dev = np.maximum(dev, np.abs(g32.astype(np.float64) * gc - g64))
         btc = G.grad_tolerance(g64, dev)
-        ill = np.abs(g64).max(axis=1) > 100.0  # the heavy tail that dominates the sums
+        # the heavy tail that dominates the sums: rows with an oracle gradient entry above 100,
+        # and rows whose gradient blows up at the KERNEL's t (t = h W + b on the matrix cores
+        # differs from numpy's by roundings; near a singular parameter that moves dt by orders
+        # of magnitude) — the first launch's dh = dt W^T shows them
+        ill = (np.abs(g64).max(axis=1) > 100.0) | (ghmax[lo:hi] > 25.0)
         ha = np.abs(hc)
         wc = ~ill
         return (hc.T @ g64, ha.T @ btc + 1e-5 * (ha.T @ np.abs(g64)), g64.sum(0), btc.sum(0) + 1e-5 * np.abs(g64).sum(0),
@@ -281,7 +292,7 @@ def test_dense_grad_full_size_against_oracle(gpu):
     ill = np.concatenate([p[8] for p in parts])
     check_bound(gW.cpu().numpy(), W_ref, bW + 1e-6, "dense grad dW C2 full batch (2^24 rows)", kind="dense_grad")
     check_bound(gb.cpu().numpy(), b_ref, bb + 1e-6, "dense grad db C2 full batch (2^24 rows)", kind="dense_grad")
-    assert ill.size < B // 5, f"{ill.size} rows with gradient entries above 100"
+    assert ill.size < B // 5, f"{ill.size} rows with gradient entries above 100 (oracle) or dh above 25 (kernel)"
     g_wc = g.clone()
     g_wc[torch.from_numpy(ill).cuda()] = 0.0
     _, _, gW2, gb2, _ = ops.chain_log_prob_dense_grad(y, h, W, b, ft, d, True, g_out=g_wc)

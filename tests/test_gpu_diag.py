@@ -56,3 +56,9 @@ def test_diag_grad_stream_bitwise_equal(gpu):
 def test_diag_flow_tile_bitwise_equal(gpu):
     res = _run("flow_tile")
     assert res["library"] == "libnfn_hip_diag.so" and res["cases"] == 48
+
+
+def test_diag_posterior_densep_bitwise_equal(gpu):
+    res = _run("densep")
+    assert res["library"] == "libnfn_hip_diag.so"
+    assert sum(v == "bitwise" for v in res.values()) == 4

@@ -184,11 +184,11 @@ def run_dense(variants, H=16, reps=20, rounds=3):
                           "rounds_ms": times[v["name"]]}), flush=True)
 
 
-def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
-    """C5 per-GPU shape with the output DenseVariational layer: fused posterior
-    (t_s formed on chip) vs the unfused path (library GEMM writes t, then the
-    posterior kernel) vs the posterior kernel alone on a resident t."""
-    ft, d = ("planar", "radial") * 5, 1
+def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3, ft=("planar", "radial") * 5, d=1, cfg="C5"):
+    """C5 per-GPU shape (or another flow stack / d) with the output DenseVariational layer:
+    fused posterior (t_s formed on chip) vs the unfused path (library GEMM writes t, then
+    the posterior kernel) vs the posterior kernel alone on a resident t; for d >= 2 also the
+    fused form on the synchronous kernel (NFN_DENSEP=0)."""
     P = ops.total_param_size(ft, d, True)
     gen = torch.Generator(device="cuda").manual_seed(1)
     y = torch.randn((B, d), generator=gen, device="cuda")
@@ -208,7 +208,16 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
         del os.environ["NFN_CHAIN_FORM"]
         return r_
 
-    fns["fused_loopform"] = loopform
+    if d == 1:
+        fns["fused_loopform"] = loopform
+    else:
+        def sync_kernel():
+            os.environ["NFN_DENSEP"] = "0"
+            r_ = ops.posterior_lse_dense(y, h, W, b, ft, d, True)
+            del os.environ["NFN_DENSEP"]
+            return r_
+
+        fns["fused_synchronous_kernel"] = sync_kernel
     stream = torch.cuda.current_stream()
     prewarm(fns["fused"])
     times = {k: [] for k in fns}
@@ -229,7 +238,7 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3):
     ref = outs["unfused_gemm_plus_posterior"]
     for k in fns:
         ms = float(np.median(times[k]))
-        print(json.dumps({"cfg": "C5", "mode": "posterior_dense", "H": H, "S": S, "B": B, "variant": k, "ms": ms,
+        print(json.dumps({"cfg": cfg, "mode": "posterior_dense", "H": H, "S": S, "B": B, "variant": k, "ms": ms,
                           "pairs_per_s": S * B / ms * 1e3,
                           "maxdiff_vs_unfused": float((outs[k] - ref).abs().max().item()),
                           "rounds_ms": times[k]}), flush=True)
@@ -482,6 +491,9 @@ def main():
         return
     if which[0] == "pdense":
         run_posterior_dense()
+        return
+    if which[0] == "pdensep":  # C3P: the d >= 2 posterior Dense kernel, prefetching vs synchronous
+        run_posterior_dense(ft=("affine",) + ("planar",) * 4 + ("radial",) * 4, d=3, cfg="C3P", rounds=4)
         return
     if which[0] == "flows":  # the per-flow Bijector path at C2: d = 1 fast-path kernel vs the generic one
         ft, d, B, _ = CFG["C2"]
