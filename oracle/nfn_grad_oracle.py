@@ -30,10 +30,26 @@ import torch
 from .nfn_oracle import param_size, total_param_size  # noqa: F401  (re-export)
 
 
+class _SoftplusTF(torch.autograd.Function):
+    """Value max(x, 0) + log1p(exp(-|x|)) (TF's SoftplusOp up to its +-13.94 cut-offs:
+    differences < 1 ulp at fp32 there), gradient sigmoid(x) everywhere (TF SoftplusGrad).
+    Autodiff through the max / abs form itself would give 1 instead of sigmoid(0) = 0.5 at
+    x = 0 exactly (clamp passes the gradient at its boundary, |x|' = sign(0) = 0) — reached
+    when a parameter product is exactly 0 (e.g. planar u = 0 on dyadic inputs)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.clamp(x, min=0) + torch.log1p(torch.exp(-torch.abs(x)))
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * torch.sigmoid(x)
+
+
 def _softplus(x: torch.Tensor) -> torch.Tensor:
-    # value of TF's SoftplusOp up to its +-13.94 cut-offs (differences < 1 ulp at
-    # fp32 there), gradient sigmoid(x) everywhere (TF SoftplusGrad).
-    return torch.clamp(x, min=0) + torch.log1p(torch.exp(-torch.abs(x)))
+    return _SoftplusTF.apply(x)
 
 
 def _planar(z, tk, d):

@@ -114,3 +114,24 @@ def test_closed_form_backward_fp32_within_tolerance(name):
         ok = np.isfinite(ref)
         ratio = np.abs(got - ref)[ok] / G.grad_tolerance(ref, dev)[ok]
         assert ratio.size == 0 or ratio.max() < 0.6, (name, float(ratio.max()))
+
+
+def test_autodiff_oracle_at_exact_zero_arguments():
+    """Softplus arguments that are exactly 0 (planar u = 0, w.u = 0; reached on dyadic
+    inputs such as the full-size Dense backward test's): the autodiff oracle's softplus
+    gradient is TF's SoftplusGrad = sigmoid(0) = 0.5 there (its max / abs value form alone
+    would autodiff to 1), so it equals the closed form at every row, exact zeros included."""
+    from analytic_grad import chain_grad
+
+    ft = ("planar", "radial") * 5
+    rng = np.random.default_rng(3)
+    h = (rng.integers(-8, 9, (2048, 16)) / 8).astype(np.float32)
+    W = (rng.integers(-16, 17, (16, 32)) / 64).astype(np.float32)
+    b = (rng.integers(-8, 9, 32) / 64).astype(np.float32)
+    t = (h @ W + b).astype(np.float32)
+    assert (t == 0).sum() > 50
+    y = rng.standard_normal((2048, 1)).astype(np.float32)
+    _, gt0, gy0 = G.chain_log_prob_grad(y, t, ft, 1, True)
+    _, gt, gy = chain_grad(y, t, ft, 1, True)
+    np.testing.assert_allclose(gt0, gt, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(gy0, gy, rtol=1e-9, atol=1e-9)
