@@ -43,6 +43,12 @@ UNITS = [
     ("grad_group_precise", "nfn_grad_group.hip", ["-DNFN_FAST=0"]),
     ("grid", "nfn_grid.hip", []),
     ("dense", "nfn_dense.hip", []),
+    # the d = 1 fused Dense kernels with the compile-time pair bodies, one unit per
+    # alternating program (hpair_types: 3 * IA + IB over planar = 0, radial = 1)
+    ("dense_hp0", "nfn_dense.hip", ["-DNFN_DENSE_HP=0"]),
+    ("dense_hp1", "nfn_dense.hip", ["-DNFN_DENSE_HP=1"]),
+    ("dense_hp3", "nfn_dense.hip", ["-DNFN_DENSE_HP=3"]),
+    ("dense_hp4", "nfn_dense.hip", ["-DNFN_DENSE_HP=4"]),
     ("dense_grad", "nfn_dense_grad.hip", []),
     ("sample", "nfn_sample.hip", []),
     ("comm", "nfn_comm.hip", []),

@@ -715,23 +715,31 @@ bool launch_pdp_h(const DenseArgs& da, hipStream_t s, int64_t* g) {
   return false;
 }
 
-template <int QH>
-void launch_pd1(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
+template <int QH, int CM>
+void launch_pd1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
   const size_t lds = (size_t)(4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
-  constexpr int CM = kChainPairs;
   auto kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1, CM>
                      : (nn == 2 ? posterior_dense1_kernel<QH, 2, CM> : (nn == 3 ? posterior_dense1_kernel<QH, 3, CM>
                                                                                 : posterior_dense1_kernel<QH, 4, CM>));
-#ifdef NFN_DIAG
-  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop)
-    kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1>
-                  : (nn == 2 ? posterior_dense1_kernel<QH, 2> : (nn == 3 ? posterior_dense1_kernel<QH, 3>
-                                                                         : posterior_dense1_kernel<QH, 4>));
-#endif
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+}
+
+#ifndef NFN_DENSE_HP
+template <int QH>
+void launch_pd1(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
+  // an alternating program (hpair_types): the compile-time pair bodies, built in their own
+  // units (nfn_dense.hip -DNFN_DENSE_HP=sel); C5 with its DenseVariational layer 0.238 ->
+  // 0.224 ms (profiles/r04/r04l_hpair_all.log)
+  int cm = env_int("NFN_CHAIN_FORM", -1);
+  if (cm < 0 && hpair_types(da.c) >= 0) cm = kChainHPair;
+  if (cm == kChainHPair && launch_dense1_hpair(hpair_types(da.c), true, da, s, grid_out)) return;
+  if (cm == kChainLoop)
+    launch_pd1_form<QH, kChainLoop>(da, s, grid_out);  // diag A/B
+  else
+    launch_pd1_form<QH, kChainPairs>(da, s, grid_out);
 }
 
 template <int DM, bool FAST>
@@ -779,28 +787,44 @@ bool launch_pd_dm(int dm, const DenseArgs& da, hipStream_t s, int64_t* g) {
   return false;
 }
 
-template <int QH>
-void launch_d1(const DenseArgs& da, size_t /*generic kernel's LDS*/, hipStream_t s, int64_t* grid_out) {
+#endif  // NFN_DENSE_HP
+
+template <int QH, int CM>
+void launch_d1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
   const size_t lds = (size_t)(4 * QH * nn * 16 + 4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
-  constexpr int CM = kChainPairs;
   auto kfn = nn <= 1 ? chain_dense1_kernel<QH, 1, CM>
                      : (nn == 2 ? chain_dense1_kernel<QH, 2, CM> : (nn == 3 ? chain_dense1_kernel<QH, 3, CM>
                                                                            : chain_dense1_kernel<QH, 4, CM>));
-#ifdef NFN_DIAG
-  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kStaticProg && nn == 2 && da.c.prog.K == kStaticK[0] &&
-      da.c.prog.types[0] == kStaticTypes[0])
-    kfn = chain_dense1_kernel<QH, 2, kStaticProg>;
-  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop)
-    kfn = nn <= 1 ? chain_dense1_kernel<QH, 1>
-                  : (nn == 2 ? chain_dense1_kernel<QH, 2> : (nn == 3 ? chain_dense1_kernel<QH, 3>
-                                                                    : chain_dense1_kernel<QH, 4>));
-#endif
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
 }
 
+#ifndef NFN_DENSE_HP
+template <int QH>
+void launch_d1(const DenseArgs& da, size_t /*generic kernel's LDS*/, hipStream_t s, int64_t* grid_out) {
+  // an alternating program (hpair_types): the compile-time pair bodies (own units), C2's
+  // Dense(H = 16) -> chain 0.445 -> 0.427 ms (profiles/r04/r04l_hpair_all.log)
+  int cm = env_int("NFN_CHAIN_FORM", -1);
+  if (cm < 0 && hpair_types(da.c) >= 0) cm = kChainHPair;
+  if (cm == kChainHPair && launch_dense1_hpair(hpair_types(da.c), false, da, s, grid_out)) return;
+#ifdef NFN_DIAG
+  if (cm == kStaticProg && (da.c.P + 15) >> 4 == 2 && da.c.prog.K == kStaticK[0] &&
+      da.c.prog.types[0] == kStaticTypes[0]) {
+    launch_d1_form<QH, kStaticProg>(da, s, grid_out);
+    return;
+  }
+  if (cm == kChainLoop) {
+    launch_d1_form<QH, kChainLoop>(da, s, grid_out);
+    return;
+  }
+#endif
+  launch_d1_form<QH, kChainPairs>(da, s, grid_out);
+}
+#endif
+
+#ifndef NFN_DENSE_HP
 template <int DM, bool FAST, int NVH>
 void launch_d(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out) {
   auto kfn = chain_dense_kernel<DM, FAST, NVH>;
@@ -844,7 +868,36 @@ bool launch_d_dm(int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s
   return false;
 }
 
+#endif  // NFN_DENSE_HP
+
 }  // namespace
+
+#ifdef NFN_DENSE_HP
+#define NFN_CAT2(a, b) a##b
+#define NFN_CAT(a, b) NFN_CAT2(a, b)
+#define NFN_DENSE_HP_FN NFN_CAT(launch_dense1_hpair_, NFN_DENSE_HP)
+// This unit: the d = 1 fused Dense kernels (forward and posterior) with the compile-time pair
+// bodies of ONE alternating program, sel = NFN_DENSE_HP = 3 * IA + IB (hpair_types).
+bool NFN_DENSE_HP_FN(bool post, const DenseArgs& da, hipStream_t s, int64_t* g) {
+  constexpr int CM = hpair_form(NFN_DENSE_HP / 3, NFN_DENSE_HP % 3, 1);
+  switch (da.H >> 2) {
+    case 1: post ? launch_pd1_form<1, CM>(da, s, g) : launch_d1_form<1, CM>(da, s, g); return true;
+    case 2: post ? launch_pd1_form<2, CM>(da, s, g) : launch_d1_form<2, CM>(da, s, g); return true;
+    case 4: post ? launch_pd1_form<4, CM>(da, s, g) : launch_d1_form<4, CM>(da, s, g); return true;
+    case 8: post ? launch_pd1_form<8, CM>(da, s, g) : launch_d1_form<8, CM>(da, s, g); return true;
+  }
+  return false;
+}
+#else
+bool launch_dense1_hpair(int sel, bool post, const DenseArgs& da, hipStream_t s, int64_t* grid) {
+  switch (sel) {
+    case 0: return launch_dense1_hpair_0(post, da, s, grid);
+    case 1: return launch_dense1_hpair_1(post, da, s, grid);
+    case 3: return launch_dense1_hpair_3(post, da, s, grid);
+    case 4: return launch_dense1_hpair_4(post, da, s, grid);
+  }
+  return false;
+}
 
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid) {
   return fast ? launch_d_dm<true>(dm, nvh, da, lds, s, grid) : launch_d_dm<false>(dm, nvh, da, lds, s, grid);
@@ -853,5 +906,6 @@ bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, h
 bool launch_posterior_dense(bool fast, int dm, const DenseArgs& da, hipStream_t s, int64_t* grid) {
   return fast ? launch_pd_dm<true>(dm, da, s, grid) : launch_pd_dm<false>(dm, da, s, grid);
 }
+#endif
 
 }  // namespace nfn

@@ -654,6 +654,45 @@ __device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, u
   return l2;
 }
 
+// chain1_fast_pairs for a program that alternates two types (IA, IB, IA, IB, ...; IA == IB
+// covers a homogeneous chain): the pair's types and offsets are compile-time, the loop body
+// one basic block (no dispatch); U pairs per trip, the remainder pair by pair.  The same
+// flow_pair1 calls on the same values as chain1_fast_pairs.
+template <int IA, int IB, int U, int ST = 1>
+__device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, int K, int P) {
+  constexpr int SA = IA == NFN_FLOW_AFFINE ? 2 : 3, SB = IB == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + SB;
+  float l2 = 0.0f;
+  int off = P;  // the current pair's block ends here
+  const int np = K >> 1;
+  int p = 0;
+#pragma unroll 1
+  for (; p + U <= np; p += U) {
+    float pa[U][3], pb[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      read3c<ST>(pa[u], row, off - u * SP - SA);
+      read3c<ST>(pb[u], row, off - u * SP - SP);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) flow_pair1<IA, IB>(z, l2, pa[u], pb[u]);
+    off -= U * SP;
+  }
+#pragma unroll 1
+  for (; p < np; ++p) {
+    float pa[3], pb[3];
+    read3c<ST>(pa, row, off - SA);
+    read3c<ST>(pb, row, off - SP);
+    flow_pair1<IA, IB>(z, l2, pa, pb);
+    off -= SP;
+  }
+  if (K & 1) {
+    float pa[3];
+    read3c<ST>(pa, row, off - SA);
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+  }
+  return l2;
+}
+
 // chain1_fast_pairs over TWO rows that share the program (two draws of one sample in the
 // posterior): one dispatch per pair of flows for both, two independent dependency chains
 // for the scheduler to interleave.  Per row the same arithmetic as chain1_fast_pairs.
@@ -703,6 +742,10 @@ __device__ __forceinline__ void chain1_fast_pairs2(float& za, float& zb, const f
 // Chain-evaluation form of the d = 1 kernels: the packed loop, two flows per dispatch,
 // or (diagnostic experiment) one compile-time program, C2's.
 constexpr int kChainLoop = 0, kStaticProg = 2, kChainPairs = 3;
+// Alternating-type programs (chain1_fast_hpairs): CM = hpair_form(IA, IB, U), U pairs per
+// loop trip.
+constexpr int kChainHPair = 8;
+constexpr int hpair_form(int ia, int ib, int u) { return kChainHPair + 9 * u + 3 * ia + ib; }
 // The pair form is bitwise the loop's.  It runs in the compute-bound d = 1 kernels
 // (posterior, fused Dense forward / backward: -5 to -11 %) and, in the streaming
 // kernels, for chains of at most this many flows (C1, K = 2: forward -18 %, backward
@@ -726,7 +769,10 @@ template <bool PACKED, int ST = 1, int CM = kChainLoop>
 __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, const ChainArgs& a) {
   const int K = a.prog.K;
   float l2 = 0.0f;  // sum of log2|det J_k|
-  if constexpr (CM == kChainPairs) {
+  if constexpr (CM >= kChainHPair) {
+    constexpr int c = CM - kChainHPair;
+    l2 = chain1_fast_hpairs<(c % 9) / 3, c % 3, c / 9, ST>(z, row, K, a.P);
+  } else if constexpr (CM == kChainPairs) {
     if (K > 0) l2 = chain1_fast_pairs<ST>(z, row, a.prog.types[0], K, a.P);
   } else if constexpr (CM == kStaticProg) {
     l2 = chain1_fast_static<kStaticTypes[0], kStaticK[0], ST>(z, row, a.P);

@@ -508,6 +508,7 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
 #ifdef NFN_DIAG
     if (cm == kStaticProg && ga.c.prog.K == kStaticK[0] && ga.c.prog.types[0] == kStaticTypes[0])
       k = chain_grad_wave_kernel<DM, FAST, NV, 1, kStaticProg>;
+    if (cm == kChainHPair && hpair_types(ga.c) == 1) k = chain_grad_wave_kernel<DM, FAST, NV, 1, hpair_form(0, 1, 1)>;
     // cache-policy A/B for the row loads and gradient stores (loop form, C2's)
     const int ntl = env_int("NFN_GRAD_NTL", 1), nts = env_int("NFN_GRAD_NTS", 1);
     if (cm == kChainLoop && (ntl == 0 || nts == 0)) {

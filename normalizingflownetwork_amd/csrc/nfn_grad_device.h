@@ -656,6 +656,90 @@ __device__ __forceinline__ float grad1_pairs(float& z, float* row, float* zh, in
   return lp;
 }
 
+// grad1_pairs for a program alternating two types (IA, IB, IA, ...: chain1_fast_hpairs):
+// the pair bodies and block offsets are compile-time, no dispatch.  The same fwd_pair1 /
+// bwd_pair1 calls on the same values as grad1_pairs.
+template <int IA, int IB, int ST, bool ODD>
+__device__ __forceinline__ float hpair_reverse(float* row, const float* zh, int zs, int K, int P, int ob0, float gl,
+                                               float a1) {
+  // flows K-1, K-2, ... in pairs; K even: (IB, IA) pairs, K odd: (IA, IB) then flow 0 (IA)
+  constexpr int TA = ODD ? IA : IB, TB = ODD ? IB : IA;
+  constexpr int SA = TA == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + (TB == NFN_FLOW_AFFINE ? 2 : 3);
+  int oba = ob0;
+  int k = K - 1;
+  float pa[3], pb[3];
+  read3c<ST>(pa, row, min(oba, P - 1));
+  read3c<ST>(pb, row, min(oba + SA, P - 1));
+  float za = zh[k * zs], zb = zh[max(k - 1, 0) * zs];
+#pragma unroll 1
+  for (; k >= 1; k -= 2) {
+    const int oban = oba + SP;
+    float pna[3], pnb[3];
+    read3c<ST>(pna, row, min(oban, P - 1));
+    read3c<ST>(pnb, row, min(oban + SA, P - 1));
+    const float zan = zh[max(k - 2, 0) * zs], zbn = zh[max(k - 3, 0) * zs];
+    bwd_pair1<TA, TB, ST>(a1, row, za, zb, pa, pb, oba, oba + SA, gl);
+    oba = oban;
+    za = zan;
+    zb = zbn;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pa[i] = pna[i];
+      pb[i] = pnb[i];
+    }
+  }
+  if constexpr (ODD) flow1_bwd<ST>(IA, za, a1, pa, row + oba * ST, gl);  // flow 0: already read
+  return a1;
+}
+
+template <int IA, int IB, int ST = 1, class Mid = NoMid>
+__device__ __forceinline__ float grad1_hpairs(float& z, float* row, float* zh, int zs, int K, int P, bool trainable,
+                                              float gl, bool want_lp, float& adj, const Mid& mid = Mid{}) {
+  constexpr int SA = IA == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + (IB == NFN_FLOW_AFFINE ? 2 : 3);
+  float l2 = 0.0f;
+  int off = P;
+  int k = 0;
+#pragma unroll 1
+  for (; k + 1 < K; k += 2) {
+    float pa[3], pb[3];
+    read3c<ST>(pa, row, off - SA);
+    read3c<ST>(pb, row, off - SP);
+    float za, zb;
+    fwd_pair1<IA, IB>(z, l2, za, zb, pa, pb, want_lp);
+    zh[k * zs] = za;
+    zh[(k + 1) * zs] = zb;
+    off -= SP;
+  }
+  if (K & 1) {
+    float pa[3];
+    read3c<ST>(pa, row, off - SA);
+    zh[(K - 1) * zs] = z;
+    if (want_lp)
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+    else
+      flow1_z(IA, z, pa);
+  }
+  const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  mid();
+  float a1;
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[ST], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    a1 = -gz;
+    row[0] = gz;
+    row[ST] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+  } else {
+    a1 = -gl * z;
+  }
+  const int ob0 = trainable ? 2 : 0;
+  adj = (K & 1) ? hpair_reverse<IA, IB, ST, true>(row, zh, zs, K, P, ob0, gl, a1)
+                : hpair_reverse<IA, IB, ST, false>(row, zh, zs, K, P, ob0, gl, a1);
+  return lp;
+}
+
 
 // Diagnostic experiment: grad1_packed for one program fixed at compile time (flow
 // inputs in registers, straight-line code).
@@ -895,6 +979,14 @@ __device__ __forceinline__ float grad_sample(float (&z)[DM], float* row, float* 
     float a1;
     const float lp1 = grad1_static<kStaticTypes[0], kStaticK[0]>(z[0], row, zh, zs, a.P, a.trainable != 0, gl,
                                                                  a.out != nullptr, a1);
+    adj[0] = a1;
+    return lp1;
+  }
+  if constexpr (DM == 1 && FAST && CM >= kChainHPair) {  // an alternating program (hpair_types)
+    float a1;
+    constexpr int c = CM - kChainHPair;
+    const float lp1 = grad1_hpairs<(c % 9) / 3, c % 3>(z[0], row, zh, zs, K, a.P, a.trainable != 0, gl,
+                                                       a.out != nullptr, a1);
     adj[0] = a1;
     return lp1;
   }

@@ -31,6 +31,20 @@ inline int env_int(const char* name, int dflt) {
 inline int env_int(const char*, int dflt) { return dflt; }
 #endif
 
+// 3 * IA + IB when the d = 1 program alternates two of (planar, radial) — IA, IB, IA, ...,
+// IA == IB for a homogeneous chain — over 2 <= K <= 16 flows; -1 otherwise.  Such programs
+// run the compile-time pair bodies (chain1_fast_hpairs / grad1_hpairs).
+inline int hpair_types(const ChainArgs& a) {
+  const int K = a.prog.K;
+  if (a.d != 1 || K < 2 || K > 16) return -1;
+  const uint32_t ty = a.prog.types[0];
+  const int ia = (int)(ty & 3u), ib = (int)((ty >> 2) & 3u);
+  if (ia > NFN_FLOW_RADIAL || ib > NFN_FLOW_RADIAL) return -1;
+  for (int k = 0; k < K; ++k)
+    if ((int)((ty >> (2 * k)) & 3u) != ((k & 1) ? ib : ia)) return -1;
+  return 3 * ia + ib;
+}
+
 // A persistent grid never exceeds the workspace's partial slots (ChainArgs::grid_cap).
 inline int64_t cap_grid(int64_t grid, const ChainArgs& a) {
   return a.grid_cap > 0 ? std::min(grid, a.grid_cap) : grid;
@@ -136,6 +150,14 @@ __host__ __device__ inline int dense1_grad_wave_floats(int P, int SH, int K) {
 // nfn_dense.hip; false if (dm, H) has no instance
 bool launch_dense(bool fast, int dm, int nvh, const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_posterior_dense(bool fast, int dm, const DenseArgs& da, hipStream_t s, int64_t* grid);
+// d = 1 fused Dense forward (post = false) / posterior (post = true) for an alternating
+// program, sel = hpair_types(da.c); each sel's kernels are their own unit (nfn_dense.hip
+// built with -DNFN_DENSE_HP=sel).  False: no kernel for this H.
+bool launch_dense1_hpair(int sel, bool post, const DenseArgs& da, hipStream_t s, int64_t* grid);
+bool launch_dense1_hpair_0(bool post, const DenseArgs& da, hipStream_t s, int64_t* grid);
+bool launch_dense1_hpair_1(bool post, const DenseArgs& da, hipStream_t s, int64_t* grid);
+bool launch_dense1_hpair_3(bool post, const DenseArgs& da, hipStream_t s, int64_t* grid);
+bool launch_dense1_hpair_4(bool post, const DenseArgs& da, hipStream_t s, int64_t* grid);
 // nfn_dense_grad.hip: returns the number of per-workgroup partials written (0 = no instance)
 int64_t launch_dense_grad(bool fast, int dm, const DenseGradArgs& g, size_t lds, int64_t max_parts, hipStream_t s);
 void launch_sum_partials(const float* part, int64_t nparts, int n, float* gW, float* gb, int nW, hipStream_t s);

@@ -11,6 +11,30 @@ namespace {
 
 constexpr bool kFast = NFN_FAST != 0;
 
+#if NFN_FAST
+// The compile-time pair bodies (chain1_fast_hpairs) of an alternating program, sel =
+// hpair_types(a).
+template <int Q, int U>
+auto posterior_hpair_kernel(int sel) {
+  switch (sel) {
+    case 0: return posterior_wave1_kernel<Q, true, hpair_form(0, 0, U)>;
+    case 1: return posterior_wave1_kernel<Q, true, hpair_form(0, 1, U)>;
+    case 3: return posterior_wave1_kernel<Q, true, hpair_form(1, 0, U)>;
+    default: return posterior_wave1_kernel<Q, true, hpair_form(1, 1, U)>;
+  }
+}
+
+template <int Q>
+auto wave1_hpair_kernel(int sel) {
+  switch (sel) {
+    case 0: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 0, 1)>;
+    case 1: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 1, 1)>;
+    case 3: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 0, 1)>;
+    default: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 1, 1)>;
+  }
+}
+#endif
+
 // d = 1 wave-tile kernel (chain_wave1_kernel) for rows of exactly Q float4.
 template <int Q>
 void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* grid_out) {
@@ -19,6 +43,10 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
 #if NFN_FAST
   if (a.prog.K <= kPairsMaxKStream && env_int("NFN_PACKED", 1) == 1)
     kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
+  // an alternating program (hpair_types): compile-time pair bodies.  C2 streams at the same
+  // rate (0.394 vs 0.393-0.403 ms) on 28 % less compute (0.269 vs 0.376 ms loads ablated,
+  // profiles/r04/r04l_hpair_all.log), and gives the posterior's bits
+  if (hpair_types(a) >= 0 && env_int("NFN_PACKED", 1) == 1) kfn = wave1_hpair_kernel<Q>(hpair_types(a));
 #ifdef NFN_DIAG
   // chain-form A/B (diag build): 0 = loop, 3 = pairs, 2 = the C2 program at compile time
   const int cm = env_int("NFN_CHAIN_FORM", -1);
@@ -26,6 +54,7 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
   if (cm == kChainPairs && a.prog.K <= 16) kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
   if (cm == kStaticProg && a.prog.K == kStaticK[0] && a.prog.types[0] == kStaticTypes[0])
     kfn = chain_wave1_kernel<true, Q, true, false, kStaticProg>;
+  if (cm == kChainHPair && hpair_types(a) >= 0) kfn = wave1_hpair_kernel<Q>(hpair_types(a));
   // LDS-DMA row fill (A/B): two LDS slots per wave, d = 1 packed loop form
   if (env_int("NFN_WAVE1_DMA", 0) == 1 && Q <= 8 && a.prog.K <= 16) {
     kfn = a.prog.K <= kPairsMaxKStream ? chain_wave1_kernel<true, Q, true, false, kChainPairs, true>
@@ -118,14 +147,23 @@ void launch_p_dm(int dm, int Q, const ChainArgs& a, int T, size_t lds, hipStream
 #if NFN_FAST
 template <int Q>
 void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) {
-  // two flows per dispatch (chain1_fast_pairs): C5 0.180 -> 0.169 ms, bitwise the same values
+  // two flows per dispatch (chain1_fast_pairs, bitwise the loop's values); an alternating
+  // program (hpair_types: C5's) as compile-time pair bodies, C5 0.182-0.186 -> 0.169 ms
+  // (profiles/r04/r04l_hpair*.log)
   auto kfn = (a.prog.K <= 16 && env_int("NFN_PACKED", 1) == 1) ? posterior_wave1_kernel<Q, true, kChainPairs>
                                                                 : posterior_wave1_kernel<Q, false>;
+  if (hpair_types(a) >= 0 && env_int("NFN_PACKED", 1) == 1) kfn = posterior_hpair_kernel<Q, 1>(hpair_types(a));
 #ifdef NFN_DIAG
-  const int cm = env_int("NFN_CHAIN_FORM", kChainPairs);
+  const int cm = env_int("NFN_CHAIN_FORM", -1);
   if (cm == kChainLoop && a.prog.K <= 16) kfn = posterior_wave1_kernel<Q, true>;
+  if (cm == kChainPairs && a.prog.K <= 16) kfn = posterior_wave1_kernel<Q, true, kChainPairs>;
   if (cm == kStaticProg && a.prog.K == kStaticK[0] && a.prog.types[0] == kStaticTypes[0])
     kfn = posterior_wave1_kernel<Q, true, kStaticProg>;
+  if (cm == kChainHPair && hpair_types(a) >= 0) {  // NFN_HPAIR_U pairs per loop trip
+    const int u = env_int("NFN_HPAIR_U", 5), sel = hpair_types(a);
+    kfn = u == 1 ? posterior_hpair_kernel<Q, 1>(sel) : u == 2 ? posterior_hpair_kernel<Q, 2>(sel)
+                                                                : posterior_hpair_kernel<Q, 5>(sel);
+  }
 #endif
   const int64_t units = a.ntiles * a.nsplit;
   const int64_t grid = cap_grid(std::min<int64_t>((units + 3) / 4, (int64_t)cu_count() * posterior_wave1_wgs_per_cu()), a);

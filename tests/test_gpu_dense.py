@@ -38,7 +38,12 @@ def _case(ft, d, H, B, seed, bias=True):
                                       (("planar", "radial") * 5, 1, 64, 777), (("affine", "planar", "radial"), 3, 8, 300),
                                       (("radial",) * 10, 1, 32, 64), (("planar", "affine"), 8, 16, 129),
                                       # d = 1 with 3 and 4 sixteen-column N tiles (P = 44, 50), H = 8 / 32
-                                      (("radial",) * 14, 1, 8, 1001), (("planar", "radial") * 8, 1, 32, 700)])
+                                      (("radial",) * 14, 1, 8, 1001), (("planar", "radial") * 8, 1, 32, 700),
+                                      # alternating / homogeneous programs of odd length (the compile-time
+                                      # pair bodies, hpair_types): (P, R) x 3 + P, (R, P) x 4 + R, P x 5
+                                      (("planar", "radial") * 3 + ("planar",), 1, 16, 500),
+                                      (("radial", "planar") * 4 + ("radial",), 1, 8, 300),
+                                      (("planar",) * 5, 1, 4, 257)])
 def test_dense_matches_oracle(math_mode, ft, d, H, B):
     from normalizingflownetwork_amd import ops
 
@@ -93,6 +98,8 @@ def _post_case(ft, d, H, B, S, seed, shared_h=False, bias=True):
     (("affine", "planar", "radial"), 3, 8, 300, 4, False),  # generic posterior kernel (d > 1)
     (("planar", "affine"), 8, 16, 129, 3, True),
     (("planar", "radial") * 2, 1, 32, 65, 1, False),     # S = 1
+    (("radial", "planar") * 3 + ("radial",), 1, 16, 300, 3, False),  # odd alternating program
+    (("planar",) * 3, 1, 8, 200, 2, False),
     # d >= 2, H <= 16, fast math: the prefetching posterior_densep_kernel (C3's flow stack at
     # d = 3, P = 60; a ragged last tile; h shared; H = 4)
     (("affine",) + ("planar",) * 4 + ("radial",) * 4, 3, 16, 777, 6, False),
@@ -165,7 +172,11 @@ def test_posterior_dense_full_size_c5_sampled(gpu):
 
 @pytest.mark.parametrize("ft,d,H,B", [(("planar", "radial") * 5, 1, 16, 1000), (("radial", "radial"), 1, 4, 333),
                                       (("affine", "planar", "radial"), 3, 8, 300), (("planar", "affine"), 8, 16, 129),
-                                      (("radial",) * 14, 1, 32, 201)])
+                                      (("radial",) * 14, 1, 32, 201),
+                                      # odd alternating / homogeneous programs (hpair_types)
+                                      (("planar", "radial") * 3 + ("planar",), 1, 16, 500),
+                                      (("radial", "planar") * 2 + ("radial",), 1, 8, 300),
+                                      (("planar",) * 5, 1, 4, 257)])
 def test_dense_grad_matches_oracle(math_mode, ft, d, H, B):
     """Backward through the fused output Dense layer + chain (nfn_chain_logprob_dense_grad_f32):
     dL/dh = dt W^T, dL/dW = h^T dt, dL/db = sum dt, dL/dy — against the autodiff oracle's dt

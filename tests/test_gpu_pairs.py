@@ -26,6 +26,11 @@ PROGRAMS = [
     ("planar", "affine", "radial", "affine", "affine", "affine"),  # K = 6, P = 16
     ("affine",) * 15,                                             # K = 15, P = 32
     ("radial", "planar") * 5,                                     # K = 10, P = 32
+    # K = 2, P = 8: every alternating (planar, radial) program of the compile-time pair
+    # bodies (hpair_types) the wave kernels take
+    ("planar", "planar"),
+    ("planar", "radial"),
+    ("radial", "planar"),
 ]
 
 

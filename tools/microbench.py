@@ -208,8 +208,15 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3, ft=("planar", 
         del os.environ["NFN_CHAIN_FORM"]
         return r_
 
+    def hpair():
+        os.environ["NFN_CHAIN_FORM"] = "8"
+        r_ = ops.posterior_lse_dense(y, h, W, b, ft, d, True)
+        del os.environ["NFN_CHAIN_FORM"]
+        return r_
+
     if d == 1:
         fns["fused_loopform"] = loopform
+        fns["fused_hpair"] = hpair
     else:
         def sync_kernel():
             os.environ["NFN_DENSEP"] = "0"
@@ -244,7 +251,7 @@ def run_posterior_dense(H=16, S=64, B=1 << 17, reps=20, rounds=3, ft=("planar", 
                           "rounds_ms": times[k]}), flush=True)
 
 
-def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False, gemm_ceiling=False):
+def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False, gemm_ceiling=False, forms=None):
     """C2 training step through the output Dense layer: the fused backward (t never
     written) vs the unfused path (library GEMM t, chain backward kernel, GEMMs for
     dh / dW and the db sum) vs the chain backward alone on a resident t."""
@@ -277,6 +284,9 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False, gemm_ceilin
     if static:
         fns = {"fused": fused, "fused_static": fused, "fused_loopform": fused}
         envs["fused_static"] = {"NFN_CHAIN_FORM": "2"}
+    if forms:  # {name: NFN_CHAIN_FORM}
+        fns = {"fused": fused, **{k: fused for k in forms}, "fused_b": fused}
+        envs.update({k: {"NFN_CHAIN_FORM": str(v)} for k, v in forms.items()})
     if gemm_ceiling:  # dh / dW MFMAs replaced by VALU touches of the same operands (NFN_DGRAD_ABLATE)
         fns = {"fused": fused, "no_dh_mfma": fused, "no_dW_mfma": fused, "no_dh_dW_mfma": fused,
                "fused_gemms_only": fused}
@@ -777,6 +787,30 @@ def main():
         run_dense([{"name": "dense1_pairs", "env": {}}, {"name": "dense1_loop", "env": {"NFN_CHAIN_FORM": 0}}])
         run_posterior_dense()
         run_dense_grad()
+        return
+    if which[0] == "hpair":  # posterior: alternating-type pair form (U pairs per trip) vs pairs / static
+        v = [{"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}}, {"name": "static", "env": {"NFN_CHAIN_FORM": 2}}]
+        for u in (1, 2, 5):
+            v.append({"name": f"hpair_u{u}", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": u}})
+        v.append({"name": "pairs_b", "env": {"NFN_CHAIN_FORM": 3}})
+        run("C5", v, reps=20, rounds=4)
+        return
+    if which[0] == "hpair_all":  # alternating-type pair form in the compute-bound d = 1 kernels
+        run("C2", [{"name": "loop", "env": {}}, {"name": "hpair", "env": {"NFN_CHAIN_FORM": 8}},
+                   {"name": "loop_compute", "env": {"NFN_ABLATE_LOADS": 1}},
+                   {"name": "hpair_compute", "env": {"NFN_CHAIN_FORM": 8, "NFN_ABLATE_LOADS": 1}},
+                   {"name": "loop_b", "env": {}}, {"name": "hpair_b", "env": {"NFN_CHAIN_FORM": 8}}], reps=20, rounds=3)
+        run_dense([{"name": "dense1_pairs", "env": {}}, {"name": "dense1_hpair", "env": {"NFN_CHAIN_FORM": 8}},
+                   {"name": "dense1_static", "env": {"NFN_CHAIN_FORM": 2}},
+                   {"name": "dense1_pairs_b", "env": {}}], rounds=4)
+        run_posterior_dense(rounds=4)
+        run_dense_grad(rounds=3, forms={"fused_hpair": 8, "fused_static": 2})
+        run_grad("C2", [{"name": "loop", "env": {}}, {"name": "hpair", "env": {"NFN_CHAIN_FORM": 8}},
+                        {"name": "static", "env": {"NFN_CHAIN_FORM": 2}},
+                        {"name": "hpair_compute", "env": {"NFN_CHAIN_FORM": 8, "NFN_ABLATE_LOADS": 1}},
+                        {"name": "loop_compute", "env": {"NFN_ABLATE_LOADS": 1}},
+                        {"name": "loop_b", "env": {}}, {"name": "hpair_b", "env": {"NFN_CHAIN_FORM": 8}}],
+                 reps=8, rounds=3)
         return
     if which[0] == "chainform":  # d = 1 chain as a packed loop, two flows per dispatch, or a compile-time program
         forms = [("loop", 0), ("pairs", 3), ("static", 2)]
