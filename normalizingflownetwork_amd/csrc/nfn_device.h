@@ -39,6 +39,13 @@
 
 #include "nfn.h"
 
+// Contraction of a * b + c into an fma only within one source expression, as written —
+// never by the backend across statements, whose choices follow the surrounding code (the
+// build default, fast-honor-pragmas).  Every kernel that inlines these evaluators — one
+// flow per loop trip, pairs, compile-time pair bodies, the grid's split form — then rounds
+// the same way, so their results agree bit for bit.  Restored at the end of this header.
+#pragma clang fp contract(on)
+
 // The memory-pipeline details (buffer descriptors, counted vmcnt waits, the agent-scope
 // partial sums across the XCDs' L2s) are validated on gfx950 only.
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
@@ -665,9 +672,29 @@ __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, 
   int off = P;  // the current pair's block ends here
   const int np = K >> 1;
   int p = 0;
+  if constexpr (U == 0) {  // one pair per trip, the next pair's parameters read first
+    float pa[3], pb[3];
+    read3c<ST>(pa, row, max(off - SA, 0));
+    read3c<ST>(pb, row, max(off - SP, 0));
+#pragma unroll 1
+    for (; p < np; ++p) {
+      off -= SP;
+      float pna[3], pnb[3];
+      read3c<ST>(pna, row, max(off - SA, 0));  // past flow 0: harmless in-row reads
+      read3c<ST>(pnb, row, max(off - SP, 0));
+      flow_pair1<IA, IB>(z, l2, pa, pb);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pa[i] = pna[i];
+        pb[i] = pnb[i];
+      }
+    }
+    if (K & 1) l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));  // already read
+    return l2;
+  }
 #pragma unroll 1
   for (; p + U <= np; p += U) {
-    float pa[U][3], pb[U][3];
+    float pa[U > 0 ? U : 1][3], pb[U > 0 ? U : 1][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       read3c<ST>(pa[u], row, off - u * SP - SA);
@@ -2152,3 +2179,5 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
 }
 
 }  // namespace nfn
+
+#pragma clang fp contract(fast)

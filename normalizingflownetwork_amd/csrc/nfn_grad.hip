@@ -503,12 +503,25 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
     if (env_int("NFN_GRAD_CAP", 0) == 1) k = chain_grad_wave_kernel<DM, FAST, NV, 4>;
   }
   if constexpr (DM == 1 && FAST) {
-    const int cm = env_int("NFN_CHAIN_FORM", ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop);
+    // an alternating program (hpair_types; at P = 4 NV only K = 2 and 10 are): the
+    // compile-time pair bodies, C2 0.861-0.870 -> 0.846-0.851 ms (profiles/r04/r04m_hpair_pf.log)
+    const int hp = (NV == 2 || NV == 8) && env_int("NFN_GRAD_CAP", 0) != 1 ? hpair_types(ga.c) : -1;
+    const int cm = env_int("NFN_CHAIN_FORM", hp >= 0 ? kChainHPair
+                                                     : (ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop));
     if (cm == kChainPairs && env_int("NFN_GRAD_CAP", 0) != 1) k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainPairs>;
+    if constexpr (NV == 2 || NV == 8) {
+      if (cm == kChainHPair && hp >= 0) {
+        switch (hp) {
+          case 0: k = chain_grad_wave_kernel<DM, FAST, NV, 1, hpair_form(0, 0, 1)>; break;
+          case 1: k = chain_grad_wave_kernel<DM, FAST, NV, 1, hpair_form(0, 1, 1)>; break;
+          case 3: k = chain_grad_wave_kernel<DM, FAST, NV, 1, hpair_form(1, 0, 1)>; break;
+          default: k = chain_grad_wave_kernel<DM, FAST, NV, 1, hpair_form(1, 1, 1)>; break;
+        }
+      }
+    }
 #ifdef NFN_DIAG
     if (cm == kStaticProg && ga.c.prog.K == kStaticK[0] && ga.c.prog.types[0] == kStaticTypes[0])
       k = chain_grad_wave_kernel<DM, FAST, NV, 1, kStaticProg>;
-    if (cm == kChainHPair && hpair_types(ga.c) == 1) k = chain_grad_wave_kernel<DM, FAST, NV, 1, hpair_form(0, 1, 1)>;
     // cache-policy A/B for the row loads and gradient stores (loop form, C2's)
     const int ntl = env_int("NFN_GRAD_NTL", 1), nts = env_int("NFN_GRAD_NTS", 1);
     if (cm == kChainLoop && (ntl == 0 || nts == 0)) {

@@ -699,20 +699,26 @@ __device__ __forceinline__ float grad1_hpairs(float& z, float* row, float* zh, i
   float l2 = 0.0f;
   int off = P;
   int k = 0;
+  float pa[3], pb[3];
+  read3c<ST>(pa, row, max(off - SA, 0));
+  read3c<ST>(pb, row, max(off - SP, 0));
 #pragma unroll 1
   for (; k + 1 < K; k += 2) {
-    float pa[3], pb[3];
-    read3c<ST>(pa, row, off - SA);
-    read3c<ST>(pb, row, off - SP);
+    off -= SP;
+    float pna[3], pnb[3];  // the next pair's parameters first (past flow 0: in-row reads)
+    read3c<ST>(pna, row, max(off - SA, 0));
+    read3c<ST>(pnb, row, max(off - SP, 0));
     float za, zb;
     fwd_pair1<IA, IB>(z, l2, za, zb, pa, pb, want_lp);
     zh[k * zs] = za;
     zh[(k + 1) * zs] = zb;
-    off -= SP;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pa[i] = pna[i];
+      pb[i] = pnb[i];
+    }
   }
-  if (K & 1) {
-    float pa[3];
-    read3c<ST>(pa, row, off - SA);
+  if (K & 1) {  // the last flow: already read
     zh[(K - 1) * zs] = z;
     if (want_lp)
       l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));

@@ -9,6 +9,10 @@
 // (tile, chunk), so HBM traffic is ~4 B per evaluation.
 #include "nfn_launch.h"
 
+// the d = 1 split form below must round as nfn_device.h's evaluators do (contraction only
+// within an expression): it then equals them bit for bit
+#pragma clang fp contract(on)
+
 namespace nfn {
 namespace {
 

@@ -24,13 +24,13 @@ auto posterior_hpair_kernel(int sel) {
   }
 }
 
-template <int Q>
+template <int Q, int U = 1>
 auto wave1_hpair_kernel(int sel) {
   switch (sel) {
-    case 0: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 0, 1)>;
-    case 1: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 1, 1)>;
-    case 3: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 0, 1)>;
-    default: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 1, 1)>;
+    case 0: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 0, U)>;
+    case 1: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 1, U)>;
+    case 3: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 0, U)>;
+    default: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 1, U)>;
   }
 }
 #endif
@@ -54,7 +54,8 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
   if (cm == kChainPairs && a.prog.K <= 16) kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
   if (cm == kStaticProg && a.prog.K == kStaticK[0] && a.prog.types[0] == kStaticTypes[0])
     kfn = chain_wave1_kernel<true, Q, true, false, kStaticProg>;
-  if (cm == kChainHPair && hpair_types(a) >= 0) kfn = wave1_hpair_kernel<Q>(hpair_types(a));
+  if (cm == kChainHPair && hpair_types(a) >= 0)
+    kfn = env_int("NFN_HPAIR_U", 1) == 0 ? wave1_hpair_kernel<Q, 0>(hpair_types(a)) : wave1_hpair_kernel<Q>(hpair_types(a));
   // LDS-DMA row fill (A/B): two LDS slots per wave, d = 1 packed loop form
   if (env_int("NFN_WAVE1_DMA", 0) == 1 && Q <= 8 && a.prog.K <= 16) {
     kfn = a.prog.K <= kPairsMaxKStream ? chain_wave1_kernel<true, Q, true, false, kChainPairs, true>
@@ -161,8 +162,9 @@ void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out
     kfn = posterior_wave1_kernel<Q, true, kStaticProg>;
   if (cm == kChainHPair && hpair_types(a) >= 0) {  // NFN_HPAIR_U pairs per loop trip
     const int u = env_int("NFN_HPAIR_U", 5), sel = hpair_types(a);
-    kfn = u == 1 ? posterior_hpair_kernel<Q, 1>(sel) : u == 2 ? posterior_hpair_kernel<Q, 2>(sel)
-                                                                : posterior_hpair_kernel<Q, 5>(sel);
+    kfn = u == 0 ? posterior_hpair_kernel<Q, 0>(sel)
+        : u == 1 ? posterior_hpair_kernel<Q, 1>(sel)
+        : u == 2 ? posterior_hpair_kernel<Q, 2>(sel) : posterior_hpair_kernel<Q, 5>(sel);
   }
 #endif
   const int64_t units = a.ntiles * a.nsplit;

@@ -795,6 +795,19 @@ def main():
         v.append({"name": "pairs_b", "env": {"NFN_CHAIN_FORM": 3}})
         run("C5", v, reps=20, rounds=4)
         return
+    if which[0] == "hpair_pf":  # one pair per trip: next pair's parameters read first (U = 0) or not (U = 1)
+        for cfg in ("C5", "C2"):
+            run(cfg, [{"name": "hpair_u1", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 1}},
+                      {"name": "hpair_u0", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 0}},
+                      {"name": "hpair_u1_compute", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 1, "NFN_ABLATE_LOADS": 1}},
+                      {"name": "hpair_u0_compute", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 0, "NFN_ABLATE_LOADS": 1}},
+                      {"name": "hpair_u1_b", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 1}},
+                      {"name": "hpair_u0_b", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 0}}], reps=20, rounds=3)
+        run_dense_grad(rounds=3, forms={"fused_hpair_prefetch": 8, "fused_static": 2})
+        run_grad("C2", [{"name": "loop", "env": {}}, {"name": "hpair_prefetch", "env": {"NFN_CHAIN_FORM": 8}},
+                        {"name": "loop_b", "env": {}}, {"name": "hpair_prefetch_b", "env": {"NFN_CHAIN_FORM": 8}}],
+                 reps=8, rounds=3)
+        return
     if which[0] == "hpair_all":  # alternating-type pair form in the compute-bound d = 1 kernels
         run("C2", [{"name": "loop", "env": {}}, {"name": "hpair", "env": {"NFN_CHAIN_FORM": 8}},
                    {"name": "loop_compute", "env": {"NFN_ABLATE_LOADS": 1}},
