@@ -503,12 +503,14 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
     if (env_int("NFN_GRAD_CAP", 0) == 1) k = chain_grad_wave_kernel<DM, FAST, NV, 4>;
   }
   if constexpr (DM == 1 && FAST) {
-    // an alternating program (hpair_types; at P = 4 NV only K = 2 and 10 are): the
-    // compile-time pair bodies, C2 0.861-0.870 -> 0.846-0.851 ms (profiles/r04/r04m_hpair_pf.log)
-    const int hp = (NV == 2 || NV == 8) && env_int("NFN_GRAD_CAP", 0) != 1 ? hpair_types(ga.c) : -1;
-    const int cm = env_int("NFN_CHAIN_FORM", hp >= 0 ? kChainHPair
-                                                     : (ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop));
+    const int cm = env_int("NFN_CHAIN_FORM", ga.c.prog.K <= kPairsMaxKStream ? kChainPairs : kChainLoop);
     if (cm == kChainPairs && env_int("NFN_GRAD_CAP", 0) != 1) k = chain_grad_wave_kernel<DM, FAST, NV, 1, kChainPairs>;
+#ifdef NFN_DIAG
+    // the compile-time pair bodies of an alternating program (hpair_types; at P = 4 NV only
+    // K = 2 and 10 are), NFN_CHAIN_FORM=8: C2 0.846-0.851 vs 0.861-0.870 ms in one process
+    // (r04m_hpair_pf.log), but as a library build 0.847-0.873 vs 0.847-0.863, and C1 0.214-0.235
+    // vs 0.219-0.227 (r04o_library_ab.txt): not adopted
+    const int hp = (NV == 2 || NV == 8) && env_int("NFN_GRAD_CAP", 0) != 1 ? hpair_types(ga.c) : -1;
     if constexpr (NV == 2 || NV == 8) {
       if (cm == kChainHPair && hp >= 0) {
         switch (hp) {
@@ -519,7 +521,6 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
         }
       }
     }
-#ifdef NFN_DIAG
     if (cm == kStaticProg && ga.c.prog.K == kStaticK[0] && ga.c.prog.types[0] == kStaticTypes[0])
       k = chain_grad_wave_kernel<DM, FAST, NV, 1, kStaticProg>;
     // cache-policy A/B for the row loads and gradient stores (loop form, C2's)
