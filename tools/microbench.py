@@ -843,6 +843,15 @@ def main():
                    {"name": "dense1_nochain", "env": {"NFN_ABLATE_FLOWS": 1}},
                    {"name": "dense1_b", "env": {}}, {"name": "generic_b", "env": {"NFN_DENSE1": 0}}])
         return
+    if which[0] == "gradc2hp":  # C2 backward with the compile-time pair bodies: fewer resident waves?
+        v = [{"name": "loop_auto", "env": {}}, {"name": "hpair_auto", "env": {"NFN_CHAIN_FORM": 8}}]
+        for wpb, wgs in ((4, (1, 2)), (2, (3, 4, 5))):
+            for wg in wgs:
+                v.append({"name": f"hpair_wpb{wpb}_wg{wg}",
+                          "env": {"NFN_CHAIN_FORM": 8, "NFN_GRAD_WPB": wpb, "NFN_WG_PER_CU": wg}})
+        v += [{"name": "loop_auto_b", "env": {}}, {"name": "hpair_auto_b", "env": {"NFN_CHAIN_FORM": 8}}]
+        run_grad("C2", v, reps=8, rounds=2)
+        return
     if which[0] == "gradc2":  # C2 backward occupancy: waves per workgroup x resident workgroups
         v = [{"name": "auto", "env": {}}]
         for wpb in (2, 4):
