@@ -386,6 +386,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
     if constexpr (CM == kStaticProg)
       lp = grad1_static<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, zh, 64, P, trainable, gl, a.out != nullptr,
                                                            adj) - corr;
+    else if constexpr (CM >= kChainHPair && (CM - kChainHPair) / 9 == 2)  // flow inputs in registers
+      lp = grad1_hpairs_regs<((CM - kChainHPair) % 9) / 3, (CM - kChainHPair) % 3, kCS>(
+               z, tl + lane, K, P, trainable, gl, a.out != nullptr, adj) - corr;
     else if constexpr (CM >= kChainHPair)
       lp = grad1_hpairs<((CM - kChainHPair) % 9) / 3, (CM - kChainHPair) % 3, kCS>(
                z, tl + lane, zh, 64, K, P, trainable, gl, a.out != nullptr, adj) - corr;
@@ -514,7 +517,8 @@ int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
 #ifdef NFN_DIAG
   if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop) kfn = chain_dense1_grad_kernel<MH, NN>;
   if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainHPair && hpair_types(g.da.c) == 1)  // (planar, radial)
-    kfn = chain_dense1_grad_kernel<MH, NN, hpair_form(0, 1, 1)>;
+    kfn = env_int("NFN_HPAIR_U", 1) == 2 ? chain_dense1_grad_kernel<MH, NN, hpair_form(0, 1, 2)>
+                                         : chain_dense1_grad_kernel<MH, NN, hpair_form(0, 1, 1)>;
   if constexpr (NN == 2) {
     if (env_int("NFN_CHAIN_FORM", kChainPairs) == kStaticProg && g.da.c.prog.K == kStaticK[0] &&
         g.da.c.prog.types[0] == kStaticTypes[0])

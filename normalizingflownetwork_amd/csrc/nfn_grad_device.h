@@ -692,6 +692,74 @@ __device__ __forceinline__ float hpair_reverse(float* row, const float* zh, int 
   return a1;
 }
 
+// grad1_hpairs with the flow inputs in registers: both passes unrolled over up to 8 pairs
+// (each guarded by the runtime pair count), so z_k needs no LDS round trip; the per-flow
+// adjoints run in the same order (K-1 .. 0) on the same values as grad1_pairs.
+template <int IA, int IB, int ST = 1>
+__device__ __forceinline__ float grad1_hpairs_regs(float& z, float* row, int K, int P, bool trainable, float gl,
+                                                   bool want_lp, float& adj) {
+  constexpr int SA = IA == NFN_FLOW_AFFINE ? 2 : 3, SB = IB == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + SB;
+  constexpr int kNP = 8;
+  float zk[2 * kNP];
+  float l2 = 0.0f;
+  const int np = K >> 1;
+#pragma unroll
+  for (int p = 0; p < kNP; ++p) {
+    zk[2 * p] = zk[2 * p + 1] = 0.0f;
+    if (p < np) {
+      float pa[3], pb[3];
+      read3c<ST>(pa, row, P - p * SP - SA);
+      read3c<ST>(pb, row, P - (p + 1) * SP);
+      fwd_pair1<IA, IB>(z, l2, zk[2 * p], zk[2 * p + 1], pa, pb, want_lp);
+    }
+  }
+  float zl = 0.0f;  // the input of flow K - 1 when K is odd
+  if (K & 1) {
+    float pa[3];
+    read3c<ST>(pa, row, P - np * SP - SA);
+    zl = z;
+    if (want_lp)
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+    else
+      flow1_z(IA, z, pa);
+  }
+  const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  float a1;
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[ST], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    a1 = -gz;
+    row[0] = gz;
+    row[ST] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+  } else {
+    a1 = -gl * z;
+  }
+  // reverse: flow K-1's block follows the base, flow k-1's follows flow k's
+  int ob = trainable ? 2 : 0;
+  if (K & 1) {
+    float pa[3];
+    read3c<ST>(pa, row, ob);
+    flow1_bwd<ST>(IA, zl, a1, pa, row + ob * ST, gl);
+    ob += SA;
+  }
+#pragma unroll
+  for (int p = kNP - 1; p >= 0; --p) {
+    if (p < np) {  // flows 2p + 1 (IB), then 2p (IA)
+      float pa[3], pb[3];
+      read3c<ST>(pb, row, ob);
+      read3c<ST>(pa, row, ob + SB);
+      flow1_bwd<ST>(IB, zk[2 * p + 1], a1, pb, row + ob * ST, gl);
+      flow1_bwd<ST>(IA, zk[2 * p], a1, pa, row + (ob + SB) * ST, gl);
+      ob += SP;
+    }
+  }
+  adj = a1;
+  return lp;
+}
+
 template <int IA, int IB, int ST = 1, class Mid = NoMid>
 __device__ __forceinline__ float grad1_hpairs(float& z, float* row, float* zh, int zs, int K, int P, bool trainable,
                                               float gl, bool want_lp, float& adj, const Mid& mid = Mid{}) {

@@ -284,9 +284,10 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False, gemm_ceilin
     if static:
         fns = {"fused": fused, "fused_static": fused, "fused_loopform": fused}
         envs["fused_static"] = {"NFN_CHAIN_FORM": "2"}
-    if forms:  # {name: NFN_CHAIN_FORM}
+    if forms:  # {name: NFN_CHAIN_FORM}; "_regs" names also set NFN_HPAIR_U=2
         fns = {"fused": fused, **{k: fused for k in forms}, "fused_b": fused}
-        envs.update({k: {"NFN_CHAIN_FORM": str(v)} for k, v in forms.items()})
+        envs.update({k: {"NFN_CHAIN_FORM": str(v), **({"NFN_HPAIR_U": "2"} if k.endswith("_regs") else {})}
+                     for k, v in forms.items()})
     if gemm_ceiling:  # dh / dW MFMAs replaced by VALU touches of the same operands (NFN_DGRAD_ABLATE)
         fns = {"fused": fused, "no_dh_mfma": fused, "no_dW_mfma": fused, "no_dh_dW_mfma": fused,
                "fused_gemms_only": fused}
@@ -300,6 +301,15 @@ def run_dense_grad(H=16, B=1 << 24, reps=20, rounds=3, static=False, gemm_ceilin
             continue
         print(json.dumps({"check": "pairs vs loop chain form", "what": name,
                           "max_abs": float((a_ - b_).abs().max().item())}), flush=True)
+    for k in (forms or {}):
+        os.environ.update(envs[k])
+        alt = [x for x in fused()]
+        for e in envs[k]:
+            del os.environ[e]
+        for name, a_, b_ in zip(("lp", "dh", "dW", "db", "dy"), alt, [x for x in fused()]):
+            if a_ is not None:
+                print(json.dumps({"check": f"{k} vs release", "what": name,
+                                  "max_abs": float((a_ - b_).abs().max().item())}), flush=True)
     ref = [x for x in fused()[1:]]
     os.environ["NFN_DENSE1_GRAD"] = "0"
     gen_out = [x for x in fused()[1:]]
@@ -842,6 +852,9 @@ def main():
                    {"name": "dense1_wg3", "env": {"NFN_WG_PER_CU": 3}},
                    {"name": "dense1_nochain", "env": {"NFN_ABLATE_FLOWS": 1}},
                    {"name": "dense1_b", "env": {}}, {"name": "generic_b", "env": {"NFN_DENSE1": 0}}])
+        return
+    if which[0] == "dgrad_regs":  # fused Dense backward: compile-time pair bodies with the flow inputs in registers
+        run_dense_grad(rounds=4, forms={"fused_hpair_regs": 8, "fused_static": 2})
         return
     if which[0] == "gradc2hp":  # C2 backward with the compile-time pair bodies: fewer resident waves?
         v = [{"name": "loop_auto", "env": {}}, {"name": "hpair_auto", "env": {"NFN_CHAIN_FORM": 8}}]
