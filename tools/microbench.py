@@ -846,6 +846,13 @@ def main():
                     v.append({"name": f"{name}_wg{wg}", "env": {"NFN_CHAIN_FORM": cm, "NFN_WG_PER_CU": wg}})
             run(cfg, v, reps=20, rounds=2)
         return
+    if which[0] == "dense_occ":  # fused Dense forward with the pair bodies: resident workgroups per CU
+        v = [{"name": "dense1_auto", "env": {}}]
+        v += [{"name": f"dense1_wg{w}", "env": {"NFN_WG_PER_CU": w}} for w in (1, 2, 3, 4)]
+        v += [{"name": "dense1_nochain", "env": {"NFN_ABLATE_FLOWS": 1}},
+              {"name": "dense1_pairs", "env": {"NFN_CHAIN_FORM": 3}}, {"name": "dense1_auto_b", "env": {}}]
+        run_dense(v, rounds=3)
+        return
     if which[0] == "dense":  # fused Dense -> chain: wave1-style pipeline vs generic, occupancy
         run_dense([{"name": "dense1", "env": {}}, {"name": "generic", "env": {"NFN_DENSE1": 0}},
                    {"name": "dense1_wg2", "env": {"NFN_WG_PER_CU": 2}},
