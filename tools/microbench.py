@@ -846,6 +846,14 @@ def main():
                     v.append({"name": f"{name}_wg{wg}", "env": {"NFN_CHAIN_FORM": cm, "NFN_WG_PER_CU": wg}})
             run(cfg, v, reps=20, rounds=2)
         return
+    if which[0] == "c1occ":  # C1 (radial x 2, 32-byte rows): stream vs chain, resident workgroups
+        v = [{"name": "auto", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+             {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}]
+        v += [{"name": f"wg{w}", "env": {"NFN_WG_PER_CU": w}} for w in (2, 3, 6, 8)]
+        v += [{"name": f"memory_only_wg{w}", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": w}} for w in (2, 6, 8)]
+        v.append({"name": "auto_b", "env": {}})
+        run("C1", v, reps=20, rounds=3)
+        return
     if which[0] == "dense_occ":  # fused Dense forward with the pair bodies: resident workgroups per CU
         v = [{"name": "dense1_auto", "env": {}}]
         v += [{"name": f"dense1_wg{w}", "env": {"NFN_WG_PER_CU": w}} for w in (1, 2, 3, 4)]
