@@ -69,12 +69,15 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
   // Resident workgroups per CU: a long chain (C2: 10 flows) keeps each wave busy
   // long enough that 2 waves per SIMD hide the streamed rows and fewer bytes in
   // flight stream faster (C2: 0.365 ms at 2 vs 0.418 at 4 per CU); a short chain
-  // (C1: 2 flows) is latency-bound and wants all 4 (0.127 vs 0.173 ms).
+  // (C1: 2 flows) in the loop form is latency-bound and wants all 4 (0.127 vs 0.173 ms); as
+  // compile-time pair bodies it is stream-bound and streams faster at 3 (C1 0.131-0.132 vs
+  // 0.142 ms, memory-only 0.131 vs 0.140; profiles/r04/r04v_c1occ.log, r04w_c1occ.log).
   int64_t grid;
+  const int wgs = a.prog.K >= 4 ? 2 : (kFast && hpair_types(a) >= 0 ? 3 : 4);
   if (env_int("NFN_WG_PER_CU", 0) > 0)
     grid = persistent_grid(kfn, T, lds, (units + teams - 1) / teams);
   else
-    grid = std::min<int64_t>((units + teams - 1) / teams, (int64_t)cu_count() * (a.prog.K >= 4 ? 2 : 4));
+    grid = std::min<int64_t>((units + teams - 1) / teams, (int64_t)cu_count() * wgs);
   grid = cap_grid(grid, a);
   *grid_out = grid;
   hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
