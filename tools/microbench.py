@@ -871,6 +871,14 @@ def main():
     if which[0] == "dgrad_regs":  # fused Dense backward: compile-time pair bodies with the flow inputs in registers
         run_dense_grad(rounds=4, forms={"fused_hpair_regs": 8, "fused_static": 2})
         return
+    if which[0] == "gradc1":  # C1 backward (radial x 2): waves per workgroup x resident workgroups
+        v = [{"name": "auto", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}}]
+        for wpb in (2, 4):
+            for wg in (1, 2, 3, 4):
+                v.append({"name": f"wpb{wpb}_wg{wg}", "env": {"NFN_GRAD_WPB": wpb, "NFN_WG_PER_CU": wg}})
+        v.append({"name": "auto_b", "env": {}})
+        run_grad("C1", v, reps=10, rounds=2)
+        return
     if which[0] == "gradc2hp":  # C2 backward with the compile-time pair bodies: fewer resident waves?
         v = [{"name": "loop_auto", "env": {}}, {"name": "hpair_auto", "env": {"NFN_CHAIN_FORM": 8}}]
         for wpb, wgs in ((4, (1, 2)), (2, (3, 4, 5))):
