@@ -51,7 +51,7 @@ CONFIGS = {
     "C3P": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 3, 1 << 17, 64),
     # configs[0]'s flow stack (radial, radial) at C2's batch, and the estimator's default
     # NormalizingFlowNetwork(n_flows=10): radial x 10 (NormalizingFlowNetwork.py:10-17)
-    "C1": (("radial", "radial"), 1, 1 << 24, None),
+    "R2": (("radial", "radial"), 1, 1 << 24, None),
     "R10": (("radial",) * 10, 1, 1 << 24, None),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -528,7 +528,7 @@ def main():
 
         flows = InverseNormalizingFlowLayer._get_bijector(t[:, 2 * d:], ft, d).bijectors
         steps = Chain([type(f)(f.params, d) for f in flows])
-        steps._fused = lambda: None
+        steps._fused = lambda x=None: None
 
         def unfused():
             steps.forward_and_log_det_jacobian(y)
@@ -594,7 +594,7 @@ def main():
             "C3": "C3: y_dim=8, affine+planar x4+radial x4, batch 2^22 per GPU",
             "C5": "C5: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=1, (planar,radial)x5",
             "C3P": "C3P: Bayes posterior, 64 draws x 2^17 samples per GPU, y_dim=3, affine+planar x4+radial x4 (P = 60)",
-            "C1": "C1: y_dim=1, (radial,radial) chain (configs[0]'s flows), batch 2^24 per GPU",
+            "R2": "R2: y_dim=1, (radial,radial) chain (configs[0]'s flows at C2's batch; not SURVEY's C1, which is B = 4096 CPU plumbing), batch 2^24 per GPU",
             "R10": "R10: y_dim=1, radial x 10 (NormalizingFlowNetwork's default), batch 2^24 per GPU",
         }[args.config]
         if args.mode == "grad":
@@ -623,7 +623,7 @@ def main():
                                "posterior_densep_kernel" if (H <= 16 and args.math == "fast") else "posterior_dense_kernel")
                 metric = f"DenseVariational(H={H})->posterior (draw, sample) evals/sec (whole node), {args.config}"
         else:
-            kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel", "C1": "chain_wave1_kernel",
+            kernel_name = {"C2": "chain_wave1_kernel", "C3": "chain_group1_kernel", "R2": "chain_wave1_kernel",
                            "R10": "chain_wave1_kernel", "C5": "posterior_wave1_kernel",
                            "C3P": "chain_persistent_kernel (posterior)"}[args.config]
             metric = ("log_prob evals/sec (whole node), 10-flow planar+radial chain, y_dim=1"

@@ -53,6 +53,9 @@
  *                             RadialFlow._forward/_forward_log_det_jacobian
  *                                                    estimators/normalizing_flows/RadialFlow.py:20-84
  *                             AffineFlow (tfp Affine) estimators/normalizing_flows/AffineFlow.py:4-9
+ *   nfn_flow_vjp_f32       <- the gradient TF's tape takes through those three bijectors'
+ *                             _forward / _forward_log_det_jacobian (PlanarFlow.py:68-80,
+ *                             RadialFlow.py:50-70, AffineFlow.py:4-9) when a loss reads them
  *   nfn_split_blocks_f32   <- the tf slices t[:, o:o+size] (copies) that _get_bijector hands each
  *                             flow                   estimators/DistributionLayers.py:267-278
  *   nfn_chain_fwd_ldj_f32  <- tfp Chain(flows).forward / .forward_log_det_jacobian as composed by
@@ -98,12 +101,13 @@ extern "C" {
 #define NFN_COMM_ID_BYTES 128
 
 /* Library version as MAJOR*10000 + MINOR*100 + PATCH.
+ *   202 (0.2.2): + nfn_flow_vjp_f32 (additive).
  *   201 (0.2.1): + nfn_split_blocks_f32 (additive; every 200 entry point unchanged).
  *   200 (0.2.0): out_sum is a device double[2] {sum, non-finite count} (was double[1]);
  *                the workspace needs no initialisation (its finishing ticket carries a
  *                per-call epoch).
  *   100 (0.1.0): first release. */
-#define NFN_ABI_VERSION 201
+#define NFN_ABI_VERSION 202
 int32_t nfn_version(void);
 
 /* Message of the last failing call on this thread ("" if none). */
@@ -222,6 +226,19 @@ int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32
 int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
                              int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out,
                              void* stream);
+
+/*
+ * One bijector's vector-Jacobian product (the backward of nfn_flow_fwd_ldj_f32): for
+ * L = sum_b <g_z[b], f(z[b])> + g_ldj[b] * log|det df/dz|(z[b]),
+ *   dz_out : (B, d) contiguous, dL/dz, may be NULL
+ *   dt_out : (B, nfn_param_size(flow_id, d)) contiguous, dL/dt_k per sample (a broadcast
+ *            t_k row still gets one gradient row per sample: the caller sums them), may be NULL
+ *   g_z    : (B, d) contiguous, or NULL for zero; g_ldj : (B,), or NULL for zero
+ *   z, t_k : as for nfn_flow_fwd_ldj_f32 (0 strides broadcast)
+ */
+int32_t nfn_flow_vjp_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k, int64_t t_rowstride,
+                         int64_t B, int32_t d, const float* g_z, const float* g_ldj, float* dz_out, float* dt_out,
+                         void* stream);
 
 /*
  * Column blocks of a parameter row, each made contiguous, in ONE pass over t:

@@ -37,6 +37,10 @@ SIGNATURES = {
         _c_int32,
         [_c_int32, _vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _vp, _vp],
     ),
+    "nfn_flow_vjp_f32": (
+        _c_int32,
+        [_c_int32, _vp, _c_int64, _vp, _c_int64, _c_int64, _c_int32, _vp, _vp, _vp, _vp, _vp],
+    ),
     "nfn_split_blocks_f32": (_c_int32, [_vp, _c_int64, _c_int64, _vp, _c_int32, _vp, _vp]),
     "nfn_chain_fwd_ldj_f32": (
         _c_int32,
@@ -94,8 +98,9 @@ NFN_E_HIP = -4
 NFN_E_COMM = -5
 NFN_COMM_ID_BYTES = 128
 # include/nfn.h NFN_ABI_VERSION: the binding's argument conventions (out_sum double[2],
-# uninitialised workspaces) and its symbol table (nfn_split_blocks_f32 since 201)
-ABI_VERSION = 201
+# uninitialised workspaces) and its symbol table (nfn_split_blocks_f32 since 201,
+# nfn_flow_vjp_f32 since 202)
+ABI_VERSION = 202
 
 _lib = None
 

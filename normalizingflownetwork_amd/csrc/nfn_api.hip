@@ -471,9 +471,10 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   const size_t slot2 = (size_t)(128 * S + a.prog.K * 128) * sizeof(float);
   if (wave_ok && use_fast_math() && d == 1 && Q <= 8 && slot2 * 2 <= (size_t)80 * 1024 &&
       env_int("NFN_GRAD_WAVE2", 0) == 1) {
-    a.ntiles = (B + 127) / 128;
+    GradArgs g2 = ga;  // a local copy: a false return leaves the caller's tiling untouched
+    g2.c.ntiles = (B + 127) / 128;
     int64_t grid = 0;
-    if (launch_grad_wave2(Q, ga, s, &grid)) return check_hip("chain_grad_wave2_kernel launch");
+    if (launch_grad_wave2(Q, g2, s, &grid)) return check_hip("chain_grad_wave2_kernel launch");
   }
 #endif
   if (wave_ok) {
@@ -923,6 +924,38 @@ int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride,
   if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
   launch_flow(use_fast_math(), dm_for(d), flow_id, z, z_bstride, t_k, t_rowstride, B, d, z_out, ldj_out, s);
   return check_hip("flow_fwd_ldj_kernel launch");
+}
+
+int32_t nfn_flow_vjp_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k, int64_t t_rowstride,
+                         int64_t B, int32_t d, const float* g_z, const float* g_ldj, float* dz_out, float* dt_out,
+                         void* stream) {
+  g_last_error.clear();
+  if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
+  const int32_t ps = param_size(flow_id, d);
+  if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id));
+  if (B < 0 || z_bstride < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
+  if (z_bstride != 0 && z_bstride < d) return fail(NFN_E_SHAPE, "z batch stride < n_dims");
+  if (t_rowstride != 0 && t_rowstride < ps) return fail(NFN_E_SHAPE, "t row stride < flow param size");
+  if (B == 0 || (!dz_out && !dt_out)) return NFN_OK;
+  if (!z || !t_k) return fail(NFN_E_NULLPTR, "z or t_k is NULL");
+  const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
+  if (nblk > 0x7fffffffLL) return fail(NFN_E_SHAPE, "batch too large");
+  FlowVjpArgs v;
+  memset(&v, 0, sizeof(v));
+  v.z = z;
+  v.z_bstride = z_bstride;
+  v.t = t_k;
+  v.t_rowstride = t_rowstride;
+  v.B = B;
+  v.g_z = g_z;
+  v.g_ldj = g_ldj;
+  v.dz = dz_out;
+  v.dt = dt_out;
+  v.flow_id = flow_id;
+  v.d = d;
+  v.ps = ps;
+  launch_flow_vjp(use_fast_math(), dm_for(d), v, reinterpret_cast<hipStream_t>(stream));
+  return check_hip("flow_vjp_kernel launch");
 }
 
 int32_t nfn_split_blocks_f32(const float* t, int64_t t_rowstride, int64_t B, const int32_t* widths, int32_t nblocks,

@@ -559,7 +559,74 @@ bool launch_wave_t(int dm, int nv, const GradArgs& ga, size_t lds_block, int wpb
   return false;
 }
 
+// The per-flow Bijector API's backward (nfn_flow_vjp_f32): one bijector's vector-Jacobian
+// product, what TF's tape takes through PlanarFlow._forward / _forward_log_det_jacobian
+// (PlanarFlow.py:68-80), RadialFlow's (RadialFlow.py:50-70) and tfp Affine's when a loss
+// reads a flow's output.  A workgroup's rows of t_k are staged in LDS (coalesced, odd
+// stride; a broadcast row is copied to every lane's row), each lane runs the flow's adjoint
+// with a = dL/dz_out and gl = dL/dldj — the adjoint overwrites its row with dL/dt_k and
+// leaves dL/dz in `a` — and the gradient rows leave through LDS as one contiguous run.
+template <int DM, bool FAST>
+__global__ void __launch_bounds__(kMaxBlock) flow_vjp_kernel(FlowVjpArgs v) {
+  extern __shared__ float lds[];
+  const int rows = blockDim.x;
+  const int tid = threadIdx.x;
+  const int SP = v.ps | 1;
+  const int d = v.d;
+  const int64_t b0 = (int64_t)blockIdx.x * rows;
+  const int nr = (int)min((int64_t)rows, v.B - b0);
+  stage_rows(lds, v.t + (v.t_rowstride == 0 ? 0 : b0 * v.t_rowstride), v.t_rowstride, nr, v.ps, SP, false);
+  __syncthreads();
+  if (tid < nr) {
+    const int64_t b = b0 + tid;
+    float z[DM], a[DM];
+    const float* zr = v.z + b * v.z_bstride;
+#pragma unroll
+    for (int j = 0; j < DM; ++j) {
+      z[j] = j < d ? zr[j] : 0.0f;
+      a[j] = (j < d && v.g_z) ? v.g_z[b * d + j] : 0.0f;
+    }
+    const float gl = v.g_ldj ? v.g_ldj[b] : 0.0f;
+    float* p = lds + tid * SP;
+    if (v.flow_id == NFN_FLOW_PLANAR)
+      planar_bwd<DM, FAST>(z, a, p, d, gl);
+    else if (v.flow_id == NFN_FLOW_RADIAL)
+      radial_bwd<DM, FAST>(z, a, p, d, gl);
+    else
+      affine_bwd<DM, FAST>(z, a, p, d, gl);
+    if (v.dz) {
+#pragma unroll
+      for (int j = 0; j < DM; ++j)
+        if (j < d) v.dz[b * d + j] = a[j];
+    }
+  }
+  __syncthreads();
+  if (v.dt) store_rows(lds, v.dt + b0 * v.ps, v.ps, nr, v.ps, SP, false);
+}
+
+template <bool FAST>
+void launch_vjp_t(int dm, const FlowVjpArgs& v, dim3 grid, size_t lds, hipStream_t s) {
+  const dim3 block(kMaxBlock);
+  switch (dm) {
+    case 1: hipLaunchKernelGGL((flow_vjp_kernel<1, FAST>), grid, block, lds, s, v); break;
+    case 2: hipLaunchKernelGGL((flow_vjp_kernel<2, FAST>), grid, block, lds, s, v); break;
+    case 4: hipLaunchKernelGGL((flow_vjp_kernel<4, FAST>), grid, block, lds, s, v); break;
+    case 8: hipLaunchKernelGGL((flow_vjp_kernel<8, FAST>), grid, block, lds, s, v); break;
+    case 16: hipLaunchKernelGGL((flow_vjp_kernel<16, FAST>), grid, block, lds, s, v); break;
+    default: hipLaunchKernelGGL((flow_vjp_kernel<32, FAST>), grid, block, lds, s, v); break;
+  }
+}
+
 }  // namespace
+
+void launch_flow_vjp(bool fast, int dm, const FlowVjpArgs& v, hipStream_t s) {
+  const int64_t nblk = (v.B + kMaxBlock - 1) / kMaxBlock;
+  const size_t lds = (size_t)kMaxBlock * (v.ps | 1) * sizeof(float);
+  if (fast)
+    launch_vjp_t<true>(dm, v, dim3((unsigned)nblk), lds, s);
+  else
+    launch_vjp_t<false>(dm, v, dim3((unsigned)nblk), lds, s);
+}
 
 void launch_grad(bool fast, int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_t s) {
   if (fast)

@@ -125,12 +125,29 @@ void launch_flow(bool fast, int dm, int32_t flow_id, const float* z, int64_t z_b
                  int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, hipStream_t s);
 // nfn_grad.hip
 void launch_grad(bool fast, int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_t s);
+// one bijector's vector-Jacobian product (nfn_flow_vjp_f32)
+struct FlowVjpArgs {
+  const float* z;
+  int64_t z_bstride;
+  const float* t;
+  int64_t t_rowstride;
+  int64_t B;
+  const float* g_z;    // (B, d) contiguous or NULL (= 0)
+  const float* g_ldj;  // (B,) or NULL (= 0)
+  float* dz;           // (B, d) contiguous or NULL
+  float* dt;           // (B, ps) contiguous or NULL
+  int32_t flow_id;
+  int32_t d;
+  int32_t ps;
+};
+void launch_flow_vjp(bool fast, int dm, const FlowVjpArgs& v, hipStream_t s);
 // wave-owned persistent form; false if (dm, nv) has no instance
 bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_block, int waves_per_block,
                       hipStream_t s, int64_t* grid);
 #ifdef NFN_DIAG
-// nfn_grad.hip (diag A/B): d = 1 fast-math backward with two samples per lane (128-row
-// wave tiles), P = 4Q with Q in {2, 4, 8}; false for other Q
+// nfn_grad2.hip (diag A/B; the unit is empty outside NFN_DIAG builds): d = 1 fast-math
+// backward with two samples per lane (128-row wave tiles), P = 4Q with Q in {2, 4, 8};
+// false for other Q
 bool launch_grad_wave2(int Q, const GradArgs& ga, hipStream_t s, int64_t* grid);
 #endif
 // nfn_grad_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance

@@ -133,8 +133,12 @@ class FlowDistribution:
 
     @property
     def bijector(self):
-        """``Invert(Chain(flows))`` over a snapshot of ``t``'s flow columns taken on first
-        access (``_get_bijector``)."""
+        """``Invert(Chain(flows))`` over a snapshot of ``t``'s flow columns taken on FIRST
+        ACCESS (``_get_bijector``), not at construction: ``log_prob`` never pays for the copy.
+        The distribution itself reads ``t`` live — ``log_prob`` / ``prob`` evaluate ``t`` as it
+        is at the call, and so does the snapshot when it is taken — so a write into ``t``
+        between construction and that first access reaches both (TF's tensors are immutable,
+        so the reference has no such window).  From then on the Chain keeps its snapshot."""
         if self._bijector is None:
             d = self._n_dims
             flow_t = _cols(self._t, 2 * d, _shape(self._t)[-1]) if self._trainable else self._t

@@ -327,7 +327,7 @@ class BaseEstimator:
             ny = torch.randn((rows, Y.shape[1]), generator=gen, device=dev) if self.y_noise_std > 0 else None
             return nx, ny
 
-        graph = None  # (graph, static idx, static x noise, static y noise)
+        graph = None  # (graph, static idx, static x noise, static y noise, its pinned workspaces)
         warm = 3  # eager steps before the capture (optimizer state, allocator pools)
         steps_done = 0
         history = {"loss": []}
@@ -339,7 +339,7 @@ class BaseEstimator:
                     idx = perm[i:i + batch_size]
                     full = idx.numel() == batch_size
                     if use_graph and full and graph is not None:
-                        g_, sidx, snx, sny = graph
+                        g_, sidx, snx, sny, _ = graph
                         sidx.copy_(idx)
                         if snx is not None:
                             snx.normal_(generator=gen)
@@ -361,7 +361,8 @@ class BaseEstimator:
                             with torch.cuda.graph(g_, stream=side):
                                 step(sidx, snx, sny)
                         torch.cuda.current_stream(dev).wait_stream(side)
-                        graph = (g_, sidx, snx, sny)
+                        # the workspaces the capture pinned live exactly as long as this graph
+                        graph = (g_, sidx, snx, sny, ops.take_graph_workspaces(side))
                         g_.replay()
                         continue
                     opt.zero_grad(set_to_none=True)

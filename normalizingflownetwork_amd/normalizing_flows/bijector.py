@@ -111,15 +111,21 @@ class Chain(Bijector):
     def bijectors(self) -> List[Bijector]:
         return self._bijectors
 
-    def _fused(self):
+    def _fused(self, x=None):
         """(flow_types in application order, base tensor, column offsets) when every
         bijector is one of the conditioned flows and their parameter blocks are column
         views of ONE device tensor (as InverseNormalizingFlowLayer._get_bijector slices
-        t): the whole chain then runs as one kernel launch.  None otherwise."""
+        t): the whole chain then runs as one kernel launch.  None otherwise — and None
+        when gradients are wanted (``x`` or a parameter block requires grad): the chain then
+        runs flow by flow through the flows' autograd op, whose backward is
+        ``nfn_flow_vjp_f32``, as TF's tape differentiates the Chain op by op."""
         from .. import ops
 
         flows = list(reversed(self._bijectors))  # application order
         if not flows or not all(hasattr(b, "flow_type") and hasattr(b, "params") for b in flows):
+            return None
+        if torch.is_grad_enabled() and (
+                (isinstance(x, torch.Tensor) and x.requires_grad) or any(b.params.requires_grad for b in flows)):
             return None
         if len({b.n_dims for b in flows}) != 1:
             return None
@@ -155,7 +161,7 @@ class Chain(Bijector):
     def forward_and_log_det_jacobian(self, x):
         """``(forward(x), forward_log_det_jacobian(x))``: one kernel launch for a chain of
         the conditioned flows (``nfn_chain_fwd_ldj_f32``), else one launch per flow."""
-        fz = self._fused()
+        fz = self._fused(x)
         if fz is not None:
             ft, t, offs, d, ops = fz
             return ops.chain_forward_ldj(ft, x, t, offs, d)
@@ -173,7 +179,7 @@ class Chain(Bijector):
         return x, fldj
 
     def _forward(self, x):
-        fz = self._fused()
+        fz = self._fused(x)
         if fz is not None:
             ft, t, offs, d, ops = fz
             return ops.chain_forward_ldj(ft, x, t, offs, d, want_ldj=False)[0]
@@ -182,7 +188,7 @@ class Chain(Bijector):
         return x
 
     def _forward_log_det_jacobian(self, x):
-        fz = self._fused()
+        fz = self._fused(x)
         if fz is not None:
             ft, t, offs, d, ops = fz
             return ops.chain_forward_ldj(ft, x, t, offs, d, want_z=False)[1]

@@ -36,14 +36,21 @@ def snapshot_rows(t):
     builds: TF's ``t[:, o:o+size]`` slices there (``DistributionLayers.py:267-278``) are copies
     of an immutable tensor, so a Chain keeps evaluating the parameters it was built from
     whatever later happens to ``t`` — including writes torch cannot see (HIP-graph replays
-    into ``t``, raw-pointer / DLPack producers).  ONE pass on the device.  The copy's rows
-    keep the 16-byte phase the one-launch Chain kernel wants: ``(-W) mod 4`` lead columns
-    (never read) put the row start on a float4 boundary, as the layer's base columns do in
-    the wide ``t`` (C2: 2 + 30 = 32 floats).  A broadcast row (stride 0) stays one row.
-    Numpy / list inputs pass through (each flow moves its own slice: already a copy)."""
+    into ``t``, raw-pointer / DLPack producers).  ONE pass on the device.  Layout: the copy
+    sits in a (B, W + lead) buffer with ``lead = (-W) mod 4`` unread columns in front of
+    each row, so the row stride is a multiple of 4 floats and every PADDED row start (the
+    view the one-launch Chain kernel streams, lead columns included) is 16-byte aligned —
+    as the layer's base columns pad the wide ``t`` (C2: 2 + 30 = 32 floats); a row's first
+    flow column itself sits ``lead`` floats after that boundary.  A broadcast row (stride 0)
+    stays one row.  Numpy / list inputs pass through (each flow moves its own slice:
+    already a copy).  When ``t`` requires grad (and grad mode is on) the copy is an autograd
+    op, so gradients of the flows' outputs reach ``t`` as TF's tape reaches the Dense output.
+    Memory: the snapshot holds B x (W + lead) floats (C2's 2^24 x 32: 2 GiB) until the flows
+    built on it are dropped."""
     if not isinstance(t, torch.Tensor) or t.dim() != 2:
         return t
-    t = t.detach()
+    if not (torch.is_grad_enabled() and t.requires_grad):
+        t = t.detach()
     B, W = int(t.shape[0]), int(t.shape[1])
     if B > 1 and t.stride(0) == 0:
         return t[:1].clone().expand(B, W)
@@ -126,16 +133,30 @@ class _ConditionedFlow(Bijector):
                 return group.blocks()[k]
         return t
 
+    def _differentiable(self, z) -> bool:
+        """A loss may read this flow's outputs: TF's tape would differentiate through the
+        flow (``PlanarFlow.py:68-80``, ``RadialFlow.py:50-70``), so the call goes through the
+        autograd op (forward kernel + ``nfn_flow_vjp_f32`` backward)."""
+        return torch.is_grad_enabled() and any(
+            isinstance(x, torch.Tensor) and x.requires_grad for x in (z, self.params))
+
     def _forward(self, z):
+        if self._differentiable(z):
+            return ops.flow_forward_ldj_diff(self.flow_type, z, self.params, self.n_dims)[0]
         z_out, _ = ops.flow_forward_ldj(self.flow_type, z, self._kernel_params(), self.n_dims, want_ldj=False)
         return z_out
 
     def _forward_log_det_jacobian(self, z):
+        if self._differentiable(z):
+            return ops.flow_forward_ldj_diff(self.flow_type, z, self.params, self.n_dims)[1]
         _, ldj = ops.flow_forward_ldj(self.flow_type, z, self._kernel_params(), self.n_dims, want_z=False)
         return ldj
 
     def forward_and_log_det_jacobian(self, z):
-        """Both results from one kernel launch."""
+        """Both results from one kernel launch (differentiable when ``z`` or the parameters
+        require grad)."""
+        if self._differentiable(z):
+            return ops.flow_forward_ldj_diff(self.flow_type, z, self.params, self.n_dims)
         return ops.flow_forward_ldj(self.flow_type, z, self._kernel_params(), self.n_dims)
 
 

@@ -75,10 +75,22 @@ _ws_lock = threading.Lock()
 # this (pooled / side streams come and go: fit's capture stream, the bench's ring).
 WORKSPACE_CACHE_ENTRIES = 8
 # Workspaces a captured HIP graph may hold the address of: handed out while their stream
-# was capturing.  Kept alive for the life of the process (graphs do not tell when they die);
-# a graph's replays write partials and the ticket there, so the block must never go back
-# to the allocator.
+# was capturing, as ((device, stream) key, workspace).  A graph's replays write partials and
+# the ticket there, so the block must not go back to the allocator while the graph lives.
+# Graphs do not tell when they die: an entry stays pinned for the life of the process unless
+# the capturing code takes it over (``take_graph_workspaces``) and keeps it next to its graph,
+# as ``estimators.fit`` does.
 _graph_workspaces: list = []
+
+
+def take_graph_workspaces(stream) -> list:
+    """Unpin and return the workspaces pinned by captures on ``stream`` (a torch stream):
+    the caller keeps them alive exactly as long as the graph(s) captured there."""
+    key = (stream.device.index, int(stream.cuda_stream))
+    with _ws_lock:
+        mine = [ws for k, ws in _graph_workspaces if k == key]
+        _graph_workspaces[:] = [(k, ws) for k, ws in _graph_workspaces if k != key]
+    return mine
 
 
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
@@ -97,8 +109,8 @@ def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < n_doubles:
             ws = torch.empty(max(2, n_doubles), dtype=torch.float64, device=device)
-        if capturing and not any(p is ws for p in _graph_workspaces):
-            _graph_workspaces.append(ws)
+        if capturing and not any(p is ws for _, p in _graph_workspaces):
+            _graph_workspaces.append((key, ws))
         _workspaces[key] = ws
         _workspaces.move_to_end(key)
         while len(_workspaces) > WORKSPACE_CACHE_ENTRIES:
@@ -635,6 +647,77 @@ def flow_forward_ldj(flow_type: str, z, t_k, n_dims: int, want_z: bool = True, w
     )
     _lib.check(rc, "nfn_flow_fwd_ldj_f32")
     return z_out, ldj
+
+
+def flow_vjp(flow_type: str, z: torch.Tensor, t_k: torch.Tensor, n_dims: int, g_z=None, g_ldj=None,
+             want_dz: bool = True, want_dt: bool = True):
+    """One bijector's vector-Jacobian product (``nfn_flow_vjp_f32``): ``(dL/dz, dL/dt_k)``
+    per sample, (B, d) and (B, p), for ``L = sum_b <g_z[b], f(z_b)> + g_ldj[b] fldj(z_b)``
+    (``g_z`` / ``g_ldj`` None => zero).  ``z`` / ``t_k`` as ``flow_forward_ldj`` takes them."""
+    dev = _device()
+    ps = param_size(flow_type, n_dims)
+    z = _prep_2d(z, n_dims, "z", dev)
+    t_k = as_device_f32(t_k, dev)
+    if t_k.dim() == 1:
+        t_k = t_k.unsqueeze(0)
+    assert t_k.shape[-1] == ps, f"{flow_type} flow needs {ps} params, got {t_k.shape[-1]}"
+    B = max(z.shape[0], t_k.shape[0])
+    assert z.shape[0] in (1, B) and t_k.shape[0] in (1, B), "incompatible batch sizes"
+    gz = gl = None
+    if g_z is not None:
+        gz = as_device_f32(g_z, dev).expand(B, n_dims).contiguous()
+    if g_ldj is not None:
+        gl = as_device_f32(g_ldj, dev).reshape(-1).expand(B).contiguous()
+    dz = torch.empty((B, n_dims), dtype=torch.float32, device=dev) if want_dz else None
+    dt = torch.empty((B, ps), dtype=torch.float32, device=dev) if want_dt else None
+    rc = _lib.load().nfn_flow_vjp_f32(
+        FLOW_IDS[flow_type], _ptr(z), _row_stride(z), _ptr(t_k), _row_stride(t_k), B, int(n_dims), _ptr(gz), _ptr(gl),
+        _ptr(dz), _ptr(dt), _stream(),
+    )
+    _lib.check(rc, "nfn_flow_vjp_f32")
+    return dz, dt
+
+
+class _FlowForwardLdj(torch.autograd.Function):
+    """One bijector's ``(forward(z), forward_log_det_jacobian(z))`` as a differentiable op:
+    forward = ``nfn_flow_fwd_ldj_f32``, backward = ``nfn_flow_vjp_f32`` (the flow is
+    recomputed there from the saved inputs).  What TF's tape differentiates through
+    ``PlanarFlow._forward`` / ``_forward_log_det_jacobian`` (``PlanarFlow.py:68-80``),
+    ``RadialFlow.py:50-70`` and tfp ``Affine``."""
+
+    @staticmethod
+    def forward(ctx, z, t_k, flow_type, n_dims):
+        ctx.set_materialize_grads(False)
+        z_out, ldj = flow_forward_ldj(flow_type, z, t_k, n_dims)
+        ctx.save_for_backward(z, t_k)
+        ctx.meta = (flow_type, int(n_dims))
+        return z_out, ldj
+
+    @staticmethod
+    def backward(ctx, g_z, g_ldj):
+        z, t_k = ctx.saved_tensors
+        flow_type, n_dims = ctx.meta
+        need_z, need_t = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if (g_z is None and g_ldj is None) or not (need_z or need_t):
+            return None, None, None, None
+        dz, dt = flow_vjp(flow_type, z, t_k, n_dims, g_z, g_ldj, want_dz=need_z, want_dt=need_t)
+        B = max(z.shape[0], t_k.shape[0])
+        if need_z and z.shape[0] == 1 and B > 1:
+            dz = dz.sum(0, keepdim=True)
+        if need_t and t_k.shape[0] == 1 and B > 1:
+            dt = dt.sum(0, keepdim=True)
+        return dz, dt, None, None
+
+
+def flow_forward_ldj_diff(flow_type: str, z, t_k, n_dims: int):
+    """Differentiable ``(forward(z), forward_log_det_jacobian(z))`` of one bijector: gradients
+    w.r.t. ``z`` and ``t_k`` flow through ``torch.autograd`` via ``nfn_flow_vjp_f32``."""
+    dev = _device()
+    z = _prep_2d(z, n_dims, "z", dev)
+    t_k = as_device_f32(t_k, dev)
+    if t_k.dim() == 1:
+        t_k = t_k.unsqueeze(0)
+    return _FlowForwardLdj.apply(z, t_k, flow_type, int(n_dims))
 
 
 def split_pays(widths: Sequence[int], row_stride: int) -> bool:

@@ -174,6 +174,49 @@ def fp32_spread(y, t, flow_types, d, trainable_base, y_mean=None, y_std=None, g_
     return gt64, gy64, dev_t, dev_y
 
 
+def flow_vjp(flow_type, z, tk, d, g_z=None, g_ldj=None, dtype=np.float64):
+    """One bijector's vector-Jacobian product: ``(dL/dz (B,d), dL/dt_k (B,p))`` for
+    ``L = sum_b <g_z[b], f(z_b)> + g_ldj[b] * fldj(z_b)`` (None => zero), through the same
+    per-flow ops as the chain (``PlanarFlow.py:43-80``, ``RadialFlow.py:44-84``, affine).
+    What TF's tape gives for a loss on ``flow.forward`` / ``forward_log_det_jacobian``.
+    Broadcast inputs (batch 1) get one gradient row per sample."""
+    tdt = torch.float64 if np.dtype(dtype) == np.float64 else torch.float32
+    B = max(np.shape(z)[0], np.shape(tk)[0])
+    p = np.shape(tk)[-1]
+    zt = torch.tensor(np.broadcast_to(np.asarray(z, dtype=dtype), (B, d)).copy(), dtype=tdt, requires_grad=True)
+    tt = torch.tensor(np.broadcast_to(np.asarray(tk, dtype=dtype), (B, p)).copy(), dtype=tdt, requires_grad=True)
+    z_new, ldj = _FLOW[flow_type](zt, tt, d)
+    L = torch.zeros((), dtype=tdt)
+    if g_z is not None:
+        L = L + (z_new * torch.tensor(np.asarray(g_z, dtype=dtype), dtype=tdt)).sum()
+    if g_ldj is not None:
+        L = L + (ldj * torch.tensor(np.asarray(g_ldj, dtype=dtype), dtype=tdt)).sum()
+    gz, gt = torch.autograd.grad(L, (zt, tt), allow_unused=True)
+    gz = torch.zeros_like(zt) if gz is None else gz
+    gt = torch.zeros_like(tt) if gt is None else gt
+    return gz.detach().numpy(), gt.detach().numpy()
+
+
+def flow_vjp_spread(flow_type, z, tk, d, g_z=None, g_ldj=None, n_perturbed=3, seed=0):
+    """``flow_vjp`` in fp64 and the fp32 restatement's largest deviation from it over the
+    inputs and ``n_perturbed`` one-ulp perturbations of them (as ``fp32_spread``).
+    Returns ``(gz64, gt64, dev_z, dev_t)``."""
+    gz64, gt64 = flow_vjp(flow_type, z, tk, d, g_z, g_ldj, np.float64)
+    rng = np.random.default_rng(seed)
+    dev_z, dev_t = np.zeros_like(gz64), np.zeros_like(gt64)
+    z32, t32 = np.asarray(z, np.float32), np.asarray(tk, np.float32)
+    for k in range(n_perturbed + 1):
+        if k == 0:
+            zk, tkk = z32, t32
+        else:
+            zk = (z32 * (1 + rng.integers(-1, 2, z32.shape) * 2.0 ** -23)).astype(np.float32)
+            tkk = (t32 * (1 + rng.integers(-1, 2, t32.shape) * 2.0 ** -23)).astype(np.float32)
+        gz32, gt32 = flow_vjp(flow_type, zk, tkk, d, g_z, g_ldj, np.float32)
+        dev_z = np.maximum(dev_z, np.abs(gz32.astype(np.float64) - gz64))
+        dev_t = np.maximum(dev_t, np.abs(gt32.astype(np.float64) - gt64))
+    return gz64, gt64, dev_z, dev_t
+
+
 def grad_tolerance(ref64: np.ndarray, dev32: np.ndarray, rel: float = 2e-5, cond_factor: float = 8.0,
                    row_scale: bool = True) -> np.ndarray:
     """Per-element bound for an fp32 gradient: ``max(rel * max(1, |ref64|, rowmax|ref64|/64),

@@ -45,12 +45,12 @@ def test_exported_symbols_are_c_linkage(native_lib):
 
 def test_version(native_lib):
     # 200: out_sum is double[2] and the workspace needs no initialisation; 201: + the
-    # additive nfn_split_blocks_f32 (include/nfn.h)
+    # additive nfn_split_blocks_f32; 202: + the additive nfn_flow_vjp_f32 (include/nfn.h)
     from normalizingflownetwork_amd import _lib
 
-    assert native_lib.nfn_version() == _lib.ABI_VERSION == 201
+    assert native_lib.nfn_version() == _lib.ABI_VERSION == 202
     hdr = open(os.path.join(REPO, "include", "nfn.h")).read()
-    assert re.search(r"#define NFN_ABI_VERSION 201\b", hdr)
+    assert re.search(r"#define NFN_ABI_VERSION 202\b", hdr)
 
 
 def _ids(*names):
@@ -193,3 +193,18 @@ def test_split_blocks_entry_point_validates(native_lib):
     w0 = (ctypes.c_int32 * 2)(3, 0)
     assert f(None, 8, 10, ctypes.cast(w0, ctypes.c_void_p), 2, None, None) == _lib.NFN_E_SHAPE
     assert f(None, 8, 0, p_w, 3, None, None) == _lib.NFN_OK              # empty batch: nothing to do
+
+
+def test_flow_vjp_entry_point_validates(native_lib):
+    from normalizingflownetwork_amd import _lib
+
+    f = native_lib.nfn_flow_vjp_f32
+    fake = 0x1000  # never dereferenced
+    assert f(9, fake, 1, fake, 3, 10, 1, None, None, fake, fake, None) == _lib.NFN_E_FLOW_ID
+    assert f(0, fake, 1, fake, 2, 10, 1, None, None, fake, fake, None) == _lib.NFN_E_SHAPE    # stride < 2d+1
+    assert f(1, fake, 1, fake, 3, 10, 0, None, None, fake, fake, None) == _lib.NFN_E_SHAPE    # n_dims 0
+    assert f(1, fake, 1, fake, 3, -1, 1, None, None, fake, fake, None) == _lib.NFN_E_SHAPE    # negative batch
+    assert f(1, None, 1, fake, 3, 10, 1, None, None, fake, fake, None) == _lib.NFN_E_NULLPTR  # NULL z
+    assert "NULL" in _lib.last_error()
+    assert f(1, fake, 1, fake, 3, 10, 1, None, None, None, None, None) == _lib.NFN_OK         # nothing requested
+    assert f(1, fake, 1, fake, 3, 0, 1, None, None, fake, fake, None) == _lib.NFN_OK          # empty batch

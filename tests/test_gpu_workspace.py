@@ -419,7 +419,7 @@ def test_graph_workspace_survives_cache_eviction(gpu):
         _, s_graph = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
     (key,) = [k for k in ops._workspaces if k[1] == int(side.cuda_stream)]
     ws = ops._workspaces[key]
-    assert any(p is ws for p in ops._graph_workspaces)
+    assert any(p is ws for _, p in ops._graph_workspaces)
     streams = [torch.cuda.Stream() for _ in range(ops.WORKSPACE_CACHE_ENTRIES + 2)]
     for st in streams:
         with torch.cuda.stream(st):
@@ -434,3 +434,34 @@ def test_graph_workspace_survives_cache_eviction(gpu):
         torch.cuda.synchronize()
         assert float(s_graph[0].item()) == pytest.approx(ref, rel=1e-12)
     assert all(float(j[0].item()) == 7.0 for j in junk)
+
+
+def test_taken_graph_workspaces_are_unpinned(gpu):
+    """A capturing caller that takes over its pinned workspaces (``ops.take_graph_workspaces``,
+    as ``fit`` keeps them next to its graph) leaves nothing pinned for that stream: repeated
+    captures on fresh streams do not grow the process-wide pin list."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d, B = ("planar", "radial") * 5, 1, 10_000
+    y = torch.randn((B, 1), device="cuda")
+    t = torch.randn((B, 32), device="cuda")
+    n0 = len(ops._graph_workspaces)
+    kept = []
+    for _ in range(3):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            _, s_graph = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
+        mine = ops.take_graph_workspaces(side)
+        assert len(mine) == 1
+        kept.append((g, s_graph, mine))
+        assert len(ops._graph_workspaces) == n0
+    for g, s_graph, _ in kept:
+        g.replay()
+    torch.cuda.synchronize()
+    ref = float(ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)[1][0].item())
+    for _, s_graph, _ in kept:
+        assert float(s_graph[0].item()) == pytest.approx(ref, rel=1e-12)

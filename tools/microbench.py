@@ -23,7 +23,7 @@ CFG = {
     "C2": (("planar", "radial") * 5, 1, 1 << 24, None),
     "C3": (("affine",) + ("planar",) * 4 + ("radial",) * 4, 8, 1 << 22, None),
     "C5": (("planar", "radial") * 5, 1, 1 << 17, 64),
-    "C1": (("radial", "radial"), 1, 1 << 24, None),
+    "R2": (("radial", "radial"), 1, 1 << 24, None),
     "K4": (("planar", "radial") * 2, 1, 1 << 24, None),
     "K6": (("planar", "radial") * 3, 1, 1 << 24, None),
     "K8": (("planar", "radial") * 4, 1, 1 << 24, None),
@@ -615,7 +615,7 @@ def main():
         return
     if which[0] == "grad2":  # d = 1 backward: two samples per lane (wave2, 128-row tiles, diag) vs one (wave)
         W2 = {"NFN_GRAD_WAVE2": 1}
-        for cfg in ("C2", "C1"):
+        for cfg in ("C2", "R2"):
             run_grad(cfg, [{"name": "wave", "env": {}}, {"name": "wave2", "env": dict(W2)},
                            {"name": "wave_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                            {"name": "wave2_memory_only", "env": dict(W2, NFN_ABLATE_FLOWS=1)},
@@ -627,7 +627,7 @@ def main():
                            {"name": "wave_b", "env": {}}, {"name": "wave2_b", "env": dict(W2)}], rounds=4)
         return
     if which[0] == "gradw1":  # d = 1 backward: straight-line buffer pipeline vs the generic wave kernel
-        for cfg in ("C2", "C1"):
+        for cfg in ("C2", "R2"):
             G = {"NFN_GRAD_WAVE1": 0}
             run_grad(cfg, [{"name": "wave1", "env": {"NFN_GRAD_WAVE1": 1}}, {"name": "generic", "env": dict(G)},
                            {"name": "wave1_memory_only", "env": {"NFN_GRAD_WAVE1": 1, "NFN_ABLATE_FLOWS": 1}},
@@ -652,7 +652,7 @@ def main():
         return
     if which[0] == "gradpc":  # d = 1 backward: producer / consumer workgroup vs the release kernel
         PC = {"NFN_GRAD_PC": 1}
-        for cfg in ("C2", "C1"):
+        for cfg in ("C2", "R2"):
             run_grad(cfg, [{"name": "release", "env": {}}, {"name": "pc", "env": dict(PC)},
                            {"name": "pc_memory_only", "env": dict(PC, NFN_ABLATE_FLOWS=1)},
                            {"name": "pc_compute_only", "env": dict(PC, NFN_ABLATE_LOADS=1)},
@@ -684,7 +684,7 @@ def main():
             v.append({"name": f"split1_wpb{wpb}_wg{wg}", "env": dict(e)})
             v.append({"name": f"split2_wpb{wpb}_wg{wg}", "env": dict(e, NFN_GRAD_SPLIT=2)})
         v += [{"name": "generic_b", "env": dict(G)}]
-        for cfg in ("C2", "C1"):
+        for cfg in ("C2", "R2"):
             run_grad(cfg, v, rounds=4)
         return
     if which[0] == "gradw1mem":  # d = 1 backward: memory-only stream vs resident waves; full at the best shapes
@@ -720,7 +720,7 @@ def main():
                            {"name": "wave_wpb4", "env": {"NFN_GRAD_WPB": 4}}])
         return
     if which[0] == "dma":  # C2 forward: register prefetch + ds_write hand-off vs LDS-DMA row fill
-        for cfg in ("C2", "C1"):
+        for cfg in ("C2", "R2"):
             run(cfg, [{"name": "regs", "env": {}}, {"name": "lds_dma", "env": {"NFN_WAVE1_DMA": 1}},
                       {"name": "regs_memonly", "env": {"NFN_ABLATE_FLOWS": 1}},
                       {"name": "lds_dma_memonly", "env": {"NFN_WAVE1_DMA": 1, "NFN_ABLATE_FLOWS": 1}}],
@@ -756,12 +756,12 @@ def main():
                      reps=10, rounds=2)
         return
     if which[0] == "gradform":  # pair form in the plain fused backward (C2, C1)
-        for cfg in ("C2", "C1"):
+        for cfg in ("C2", "R2"):
             run_grad(cfg, [{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}},
                            {"name": "loop_compute", "env": {"NFN_ABLATE_LOADS": 1}},
                            {"name": "pairs_compute", "env": {"NFN_CHAIN_FORM": 3, "NFN_ABLATE_LOADS": 1}}],
                      reps=10, rounds=2)
-        run(cfg="C1", variants=[{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}}])
+        run(cfg="R2", variants=[{"name": "loop", "env": {}}, {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}}])
         return
     if which[0] == "dgradcmp":  # pair vs loop chain form in the fused Dense backward: where do dh / dW differ
         ft, d, H = ("planar", "radial") * 5, 1, 16
@@ -835,6 +835,22 @@ def main():
                         {"name": "loop_b", "env": {}}, {"name": "hpair_b", "env": {"NFN_CHAIN_FORM": 8}}],
                  reps=8, rounds=3)
         return
+    if which[0] == "c2form5":  # round 5: C2 / R10 streaming forward, pair bodies vs loop, occupancy
+        for cfg in which[1:] or ["C2", "R10"]:
+            v = [{"name": "auto_hpair", "env": {}},
+                 {"name": "hpair_wg3", "env": {"NFN_WG_PER_CU": 3}},
+                 {"name": "hpair_wg4", "env": {"NFN_WG_PER_CU": 4}},
+                 {"name": "hpair_u0", "env": {"NFN_CHAIN_FORM": 8, "NFN_HPAIR_U": 0}},
+                 {"name": "loop", "env": {"NFN_CHAIN_FORM": 0}},
+                 {"name": "loop_wg3", "env": {"NFN_CHAIN_FORM": 0, "NFN_WG_PER_CU": 3}},
+                 {"name": "pairs", "env": {"NFN_CHAIN_FORM": 3}},
+                 {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
+                 {"name": "memory_only_wg3", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": 3}},
+                 {"name": "hpair_compute", "env": {"NFN_ABLATE_LOADS": 1}},
+                 {"name": "loop_compute", "env": {"NFN_CHAIN_FORM": 0, "NFN_ABLATE_LOADS": 1}},
+                 {"name": "auto_hpair_b", "env": {}}]
+            run(cfg, v, reps=20, rounds=3)
+        return
     if which[0] == "chainform":  # d = 1 chain as a packed loop, two flows per dispatch, or a compile-time program
         forms = [("loop", 0), ("pairs", 3), ("static", 2)]
         for cfg in ("C2", "C5"):
@@ -852,7 +868,7 @@ def main():
         v += [{"name": f"wg{w}", "env": {"NFN_WG_PER_CU": w}} for w in (2, 3, 6, 8)]
         v += [{"name": f"memory_only_wg{w}", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": w}} for w in (2, 6, 8)]
         v.append({"name": "auto_b", "env": {}})
-        run("C1", v, reps=20, rounds=3)
+        run("R2", v, reps=20, rounds=3)
         return
     if which[0] == "dense_occ":  # fused Dense forward with the pair bodies: resident workgroups per CU
         v = [{"name": "dense1_auto", "env": {}}]
@@ -877,7 +893,7 @@ def main():
             for wg in (1, 2, 3, 4):
                 v.append({"name": f"wpb{wpb}_wg{wg}", "env": {"NFN_GRAD_WPB": wpb, "NFN_WG_PER_CU": wg}})
         v.append({"name": "auto_b", "env": {}})
-        run_grad("C1", v, reps=10, rounds=2)
+        run_grad("R2", v, reps=10, rounds=2)
         return
     if which[0] == "gradc2hp":  # C2 backward with the compile-time pair bodies: fewer resident waves?
         v = [{"name": "loop_auto", "env": {}}, {"name": "hpair_auto", "env": {"NFN_CHAIN_FORM": 8}}]
@@ -1030,7 +1046,7 @@ def main():
              {"name": "wave1_memory_only", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": 2}},
              {"name": "wave1_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
              {"name": "wave1_b", "env": {}}]
-        for cfg in which[1:] or ["C2", "C1"]:
+        for cfg in which[1:] or ["C2", "R2"]:
             run(cfg, v)
         return
     if which[0] == "c5":  # posterior: posterior_wave1_kernel (default) vs the generic persistent kernel
@@ -1121,7 +1137,7 @@ def main():
              {"name": "g4_memory_only", "env": {"NFN_ABLATE_FLOWS": 1, "NFN_WG_PER_CU": 2}},
              {"name": "g4_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
              {"name": "g4_b", "env": {}}, {"name": "g1_b", "env": {"NFN_UNIT_TILES": 1}}]
-        for cfg in which[1:] or ["C2", "C1"]:
+        for cfg in which[1:] or ["C2", "R2"]:
             run(cfg, v)
         return
     if which[0] == "mem":  # memory-path study on C2
@@ -1160,7 +1176,7 @@ def main():
         {"name": "rows128_ablate", "env": {"NFN_TILE_ROWS": 128, "NFN_ABLATE_FLOWS": 1}},
     ]
     for cfg in which:
-        run(cfg, base if cfg in ("C2", "C1") else [b for b in base if b["name"] in ("auto", "tile", "precise", "ablate_flows")])
+        run(cfg, base if cfg in ("C2", "R2") else [b for b in base if b["name"] in ("auto", "tile", "precise", "ablate_flows")])
 
 
 if __name__ == "__main__":
