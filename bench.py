@@ -249,13 +249,14 @@ def spawn_ranks(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
-def nfn_environment() -> dict:
+def nfn_environment(allow_ablation: bool = False) -> dict:
     """Every NFN_* variable in the environment (recorded in the JSON line).  The release
     library reads only NFN_MATH (overridden by --math); the tuning / ablation knobs exist
-    only in the NFN_DIAG build, and an ablation knob in the environment aborts the bench."""
+    only in the NFN_DIAG build, and an ablation knob in the environment aborts the bench
+    (unless --diag: an A/B study with the diagnostic library, never a reported line)."""
     env = {k: v for k, v in os.environ.items() if k.startswith("NFN_")}
     bad = [k for k in env if k.startswith("NFN_ABLATE")]
-    if bad:
+    if bad and not allow_ablation:
         raise SystemExit(f"refusing to benchmark with ablation knobs set: {bad}")
     return env
 
@@ -272,6 +273,9 @@ def main():
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="override the per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--diag", action="store_true",
+                    help="bind libnfn_hip_diag.so (NFN_* knobs, e.g. NFN_ABLATE_FLOWS=1): A/B studies only, "
+                         "never a reported line")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--math", default="fast", choices=["fast", "precise"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -305,7 +309,11 @@ def main():
                     help="N > 1 mean all-reduce: torch.distributed, or the library's own RCCL "
                          "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
     args = ap.parse_args()
-    nfn_env = nfn_environment()
+    if args.diag:  # measurement tool only: the NFN_DIAG library reads NFN_* ablation / tuning knobs
+        from normalizingflownetwork_amd import _lib
+
+        _lib.use_diagnostic_build()
+    nfn_env = nfn_environment(allow_ablation=args.diag)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
 
@@ -687,6 +695,7 @@ def main():
             "nonfinite_log_prob": nonfinite,
             "unfused_ms": unfused_ms,
             "nfn_env": nfn_env,
+            **({"library": "libnfn_hip_diag.so (--diag: A/B study, not a reported line)"} if args.diag else {}),
         }
         print(json.dumps(line), flush=True)
     if native is not None:

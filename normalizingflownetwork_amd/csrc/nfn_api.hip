@@ -232,6 +232,8 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
   a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
+  a.pace = env_int("NFN_PACE", 0);
+  a.pace_rand = env_int("NFN_PACE_RAND", 0);
   a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // measured +1-2% (C2, C5); 2 = + static split
   {
     const int32_t rc = check_chain_args(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, P, y_mean, y_std, out_sum,
@@ -503,6 +505,7 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMM + streaming alone
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // diagnostic: compute-only (first tile re-read)
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");
@@ -564,6 +567,7 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMMs + streaming alone
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // diagnostic: compute-only (first tile re-read)
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
@@ -632,6 +636,7 @@ int32_t run_dense_grad(const float* y, int64_t y_bstride, const float* h, int64_
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMMs + streaming alone
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // diagnostic: compute-only (first tile re-read)
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");

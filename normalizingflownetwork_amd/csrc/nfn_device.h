@@ -111,6 +111,8 @@ struct ChainArgs {
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
+  int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
+  int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace dependent fma (< 0)
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
@@ -261,28 +263,28 @@ __device__ __forceinline__ float softplus_alpha(float x) {
   }
 }
 
-// tanh with RELATIVE accuracy everywhere (<= 1.7 ulp, 0.27 on average; tools/kernel_emu.py
-// with correctly rounded v_exp / v_rcp).  An absolute error of ~1e-7 is a large relative one
+// tanh with RELATIVE accuracy everywhere.  An absolute error of ~1e-7 is a large relative one
 // as a -> 0; a planar step multiplies tanh by u_hat, which reaches ~1 / |w| when w -> 0
 // (u_hat ~ m / w), so the absolute error became a z error of ~1e-7 / |w| (C2 full batch:
 // log_prob off by up to 2e-4 on 2e-5 of the samples, tests/test_gpu_fullbatch.py).
-// Below |a| = 0.55 an odd minimax polynomial (tanh(a) / a - 1 as five terms in a^2, fitted
-// for relative error on [0, 0.55]: <= 0.75 ulp); above it 1 - 2 / (1 + e^{2|a|}) with the
-// sign copied back (<= 2.2 ulp at 0.55, 1.3 past 1; e^{2|a|} -> inf saturates to 1).  The
-// round-3 form (Taylor to a^9 below 0.3, 1 - 2 / (1 + e^{2a}) at signed a) reached 5.2 ulp on
-// the negative side, where 2 / (1 + e^{2a}) > 1 has twice the ulp; this one costs two VALU
-// more per evaluation (measured: C2 +1.8 %, C5 +1.3 %, profiles/r04/r04c_*).
+// Below |a| = 0.3 an odd polynomial (tanh(a) / a - 1 as three terms in a^2, fitted for relative
+// error on [0, 0.3]: <= 0.69 ulp, 0.26 on average); above it 1 - 2 / (1 + e^{2|a|}) with the
+// sign copied back (<= 2.9 ulp on [0.3, 1), <= 1.2 past 1; e^{2|a|} -> inf saturates to 1; ulp
+// figures with correctly rounded v_exp / v_rcp, both signs alike).  Evaluating the exp form
+// at |a| is what round 4's accuracy gain came from: round 3 evaluated it at signed a, where
+// 2 / (1 + e^{2a}) > 1 has twice the ulp (5.2 ulp).  Round 4's five-term polynomial on [0, 0.55]
+// bought nothing over this one in the fp32 emulation of the C2 chain (tools/kernel_emu.py: 200
+// vs 206 of 2^21 samples beyond 3e-6 relative, 5 vs 5 beyond 1e-5) and cost two VALU per planar
+// flow, which the C2 stream pays for (profiles/r05/).
 __device__ __forceinline__ float tanh_fast(float a) {
   const float x = fabsf(a);
   const float E = __builtin_amdgcn_exp2f(x * (2.0f * kLog2e));
   const float te = copysignf(1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f)), a);
   const float a2 = a * a;
-  float p = fmaf(a2, -0.0062827035f, 0.021077914f);
-  p = fmaf(a2, p, -0.053853896f);
-  p = fmaf(a2, p, 0.13332602f);
-  p = fmaf(a2, p, -0.3333332f);
+  float p = fmaf(a2, -0.050372913f, 0.13314915f);
+  p = fmaf(a2, p, -0.33333063f);
   const float tp = fmaf(a * a2, p, a);
-  return x < 0.55f ? tp : te;
+  return x < 0.3f ? tp : te;
 }
 
 template <bool FAST>
@@ -1441,6 +1443,21 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     }
     pend_v = lp;
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+#ifdef NFN_DIAG
+    // pacing study: pace > 0 sleeps (s_sleep 1, ~64 cycles each), pace < 0 issues -pace x 16
+    // dependent v_fma_f32 whose result is kept (busy VALU, no memory)
+    for (int i = 0; i < a.pace; ++i) __builtin_amdgcn_s_sleep(1);
+    if (a.pace_rand > 0) {  // a pseudo-random number of s_sleep(1) in [0, pace_rand) per (wave, tile)
+      const uint32_t h = (uint32_t)tile * 2654435761u ^ (uint32_t)(blockIdx.x * 8 + wid) * 40503u;
+      const int n = (int)((h >> 13) % (uint32_t)a.pace_rand);
+      for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
+    }
+    if (a.pace < 0) {
+      float x = lp;
+      for (int i = 0; i < -16 * a.pace; ++i) x = fmaf(x, 0.999f, 0.5f);
+      asm volatile("" ::"v"(x));
+    }
+#endif
     wave_lds_sync();  // this tile's LDS reads done before the next writes
   }
   flush();

@@ -43,10 +43,13 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
 #if NFN_FAST
   if (a.prog.K <= kPairsMaxKStream && env_int("NFN_PACKED", 1) == 1)
     kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
-  // an alternating program (hpair_types): compile-time pair bodies.  C2 streams at the same
-  // rate (0.394 vs 0.393-0.403 ms) on 28 % less compute (0.269 vs 0.376 ms loads ablated,
-  // profiles/r04/r04l_hpair_all.log), and gives the posterior's bits
-  if (hpair_types(a) >= 0 && env_int("NFN_PACKED", 1) == 1) kfn = wave1_hpair_kernel<Q>(hpair_types(a));
+  // a short alternating program (hpair_types, K <= kPairsMaxKStream: C1 / R2): compile-time
+  // pair bodies.  Longer chains (C2, R10) stay on the packed loop, as in round 3: in the bench
+  // harness C2 streams faster with the loop's chain than with the pair bodies' lighter one
+  // (0.388 vs 0.394 ms; R10 0.378 vs 0.391 in the one-process microbench), and the loop form
+  // even beats the kernel's own memory-only time (profiles/r05/r05m_*)
+  if (hpair_types(a) >= 0 && a.prog.K <= kPairsMaxKStream && env_int("NFN_PACKED", 1) == 1)
+    kfn = wave1_hpair_kernel<Q>(hpair_types(a));
 #ifdef NFN_DIAG
   // chain-form A/B (diag build): 0 = loop, 3 = pairs, 2 = the C2 program at compile time
   const int cm = env_int("NFN_CHAIN_FORM", -1);
