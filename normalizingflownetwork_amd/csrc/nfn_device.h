@@ -112,7 +112,7 @@ struct ChainArgs {
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
   int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
-  int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace dependent fma (< 0)
+  int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace fma in 8 independent chains (< 0)
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
@@ -1445,17 +1445,23 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
 #ifdef NFN_DIAG
     // pacing study: pace > 0 sleeps (s_sleep 1, ~64 cycles each), pace < 0 issues -pace x 16
-    // dependent v_fma_f32 whose result is kept (busy VALU, no memory)
+    // v_fma_f32 in eight independent chains whose results are kept (busy VALU, no memory)
     for (int i = 0; i < a.pace; ++i) __builtin_amdgcn_s_sleep(1);
     if (a.pace_rand > 0) {  // a pseudo-random number of s_sleep(1) in [0, pace_rand) per (wave, tile)
       const uint32_t h = (uint32_t)tile * 2654435761u ^ (uint32_t)(blockIdx.x * 8 + wid) * 40503u;
       const int n = (int)((h >> 13) % (uint32_t)a.pace_rand);
       for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
     }
-    if (a.pace < 0) {
-      float x = lp;
-      for (int i = 0; i < -16 * a.pace; ++i) x = fmaf(x, 0.999f, 0.5f);
-      asm volatile("" ::"v"(x));
+    if (a.pace < 0) {  // -pace x 16 fma in 8 independent chains (the VALU busy, not waiting)
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = lp + (float)j;
+      for (int i = 0; i < -2 * a.pace; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = fmaf(x[j], 0.999f, 0.5f);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(x[j]));
     }
 #endif
     wave_lds_sync();  // this tile's LDS reads done before the next writes
