@@ -111,6 +111,7 @@ struct ChainArgs {
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
+  int32_t store_aux;   // diagnostic (NFN_STORE_AUX, diag builds): the forward kernels' log_prob store cache policy (store_out32)
   int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
   int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace fma in 8 independent chains (< 0)
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
@@ -1311,6 +1312,31 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+// The per-tile log_prob store of the streaming forward kernels (wave1, posterior_wave1,
+// group1).  Cache policy kOutAux = sc1 (aux bits 16: write-through, the line is dropped from
+// the XCD's L2) instead of non-temporal (2): in the bench harness the C2 stream with the
+// compile-time pair bodies runs 0.378-0.380 ms with sc1 stores against 0.389-0.391 with nt
+// (three boxes, profiles/r05/r05u / r05v / r05w_*), C3 -0.5 %, C5 unchanged; the memory-only
+// form gains the same 2.5 %.  (The backward's gradient stores stay nt: a backward-shaped stream
+// gains nothing from sc1, r05w_mixed_stream.log.)  The diagnostic build takes NFN_STORE_AUX
+// (a.store_aux: 0, 2, 16 or 18; -1 = kOutAux) for A/B studies.
+constexpr int kOutAux = 16;
+__device__ __forceinline__ void store_out32(float v, __amdgpu_buffer_rsrc_t r, int off, const ChainArgs& a) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+#ifdef NFN_DIAG
+  switch (a.store_aux) {
+    case 0: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 0); return;
+    case 2: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 2); return;
+    case 16: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 16); return;
+    case 18: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 18); return;
+    default: break;
+  }
+#else
+  (void)a;
+#endif
+  __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, kOutAux);
+}
+
 // FWD: the Bijector API's Chain forward + forward_log_det_jacobian instead of log_prob
 // (nfn_chain_fwd_ldj_f32 over the layer's flow blocks; needs FAST and PACKED): z_K goes to
 // a.z_out and sum_k log|det J_k| to a.out; no base density, no partial sums.
@@ -1388,7 +1414,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0), pend_rz = tile_rsrc(a.z_out, 0);
   float pend_v = 0.0f, pend_z = 0.0f;
   auto flush = [&]() {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+    store_out32(pend_v, pend_r, lane * 4, a);
     if constexpr (FWD)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_z), pend_rz, lane * 4, 0, kNT);
   };
@@ -1541,7 +1567,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) posterior_wave1_kernel(ChainArgs
   float pend_v = 0.0f, pend_m = 0.0f;
   auto flush = [&]() {
     if (nsp == 1)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+      store_out32(pend_v, pend_r, lane * 4, a);
     else
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(pend_m, pend_v)), pend_r,
                                             lane * 8, 0, kNT);
@@ -2163,7 +2189,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   issue(u0);
   // an (empty) store behind the first prefetch too: every path into the loop then
   // ends [loads][store] and the hand-off waits with vmcnt(1), not vmcnt(0)
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  store_out32(pend_v, pend_r, lane * 4, a);
   for (int64_t tile = u0; tile < a.ntiles; tile += ustep) {
     const int64_t b0 = tile * R;
     const int64_t nr = max((int64_t)0, min((int64_t)R, a.B - b0));
@@ -2175,7 +2201,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
     for (int i = 0; i < DPL; ++i) z[i] = norm ? f_div<FAST>(ybuf[i] - ymean[i], yrstd[i]) : ybuf[i];
     wave_lds_sync();
     issue(tile + ustep);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+    store_out32(pend_v, pend_r, lane * 4, a);
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     const float lp = eval_chain_gd<G, DPL, FAST, FULL, FWD>(z, tl + sl * S, a, j) - corr;
     wave_lds_sync();  // this tile's LDS reads done before the next writes
@@ -2195,7 +2221,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
     pend_v = __shfl(lp, (lane * G) & 63);
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? (int)nr * 4 : 0);
   }
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_v), pend_r, lane * 4, 0, kNT);
+  store_out32(pend_v, pend_r, lane * 4, a);
   if (a.partials) {
     write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }

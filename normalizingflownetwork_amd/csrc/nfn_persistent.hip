@@ -43,13 +43,12 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
 #if NFN_FAST
   if (a.prog.K <= kPairsMaxKStream && env_int("NFN_PACKED", 1) == 1)
     kfn = chain_wave1_kernel<true, Q, true, false, kChainPairs>;
-  // a short alternating program (hpair_types, K <= kPairsMaxKStream: C1 / R2): compile-time
-  // pair bodies.  Longer chains (C2, R10) stay on the packed loop, as in round 3: in the bench
-  // harness C2 streams faster with the loop's chain than with the pair bodies' lighter one
-  // (0.388 vs 0.394 ms; R10 0.378 vs 0.391 in the one-process microbench), and the loop form
-  // even beats the kernel's own memory-only time (profiles/r05/r05m_*)
-  if (hpair_types(a) >= 0 && a.prog.K <= kPairsMaxKStream && env_int("NFN_PACKED", 1) == 1)
-    kfn = wave1_hpair_kernel<Q>(hpair_types(a));
+  // an alternating program (hpair_types): compile-time pair bodies.  With the log_prob stores
+  // write-through (kOutAux) they stream C2 at 0.378-0.380 ms against 0.395-0.400 for the packed
+  // loop on three boxes (bench harness, profiles/r05/r05u / r05v / r05w_*; round 3's loop
+  // library 0.380 on the same box); with non-temporal stores the two forms traded places box to
+  // box (r05m vs r05u), which is why round 5 first moved C2 back to the loop
+  if (hpair_types(a) >= 0 && env_int("NFN_PACKED", 1) == 1) kfn = wave1_hpair_kernel<Q>(hpair_types(a));
 #ifdef NFN_DIAG
   // chain-form A/B (diag build): 0 = loop, 3 = pairs, 2 = the C2 program at compile time
   const int cm = env_int("NFN_CHAIN_FORM", -1);

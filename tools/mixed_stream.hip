@@ -35,7 +35,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes)
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
 }
 
-template <int K, int PF>
+template <int K, int PF, int SPOL = 2>
 __global__ void __launch_bounds__(256) mixed_kernel(const float* __restrict__ t, const float* __restrict__ y,
                                                     const float* __restrict__ g, float* __restrict__ gt,
                                                     float* __restrict__ gy, int64_t nunits) {
@@ -66,8 +66,8 @@ __global__ void __launch_bounds__(256) mixed_kernel(const float* __restrict__ t,
     for (int j = 0; j < K; ++j) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        __builtin_amdgcn_raw_buffer_store_b128(cur[j][k], rt, lane * 16, j * 8192 + k * 1024, 2);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dy[j]), ry, lane * 4, j * 256, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(cur[j][k], rt, lane * 16, j * 8192 + k * 1024, SPOL);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dy[j]), ry, lane * 4, j * 256, SPOL);
     }
   };
   if (PF) issue(w0);
@@ -86,13 +86,13 @@ __global__ void __launch_bounds__(256) mixed_kernel(const float* __restrict__ t,
   }
 }
 
-template <int K, int PF>
+template <int K, int PF, int SPOL = 2>
 void measure(const float* t, const float* y, const float* g, float* gt, float* gy, int64_t ntiles, int cus,
              double bytes) {
   const int64_t nunits = ntiles / K;
   int occ = 0;
-  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(mixed_kernel<K, PF>), 256, 0));
-  printf("K=%d PF=%d (max %d wg/CU = %2d waves/CU) |", K, PF, occ, 4 * occ);
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(mixed_kernel<K, PF, SPOL>), 256, 0));
+  printf("K=%d PF=%d stores aux %2d (max %d wg/CU = %2d waves/CU) |", K, PF, SPOL, occ, 4 * occ);
   for (int wpc = 1; wpc <= 4; ++wpc) {
     if (wpc > occ) {
       printf(" wg/CU=%d       -            |", wpc);
@@ -105,7 +105,7 @@ void measure(const float* t, const float* y, const float* g, float* gt, float* g
     std::vector<float> ts;
     for (int r = 0; r < 15; ++r) {
       CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL((mixed_kernel<K, PF>), dim3(grid), dim3(256), 0, 0, t, y, g, gt, gy, nunits);
+      hipLaunchKernelGGL((mixed_kernel<K, PF, SPOL>), dim3(grid), dim3(256), 0, 0, t, y, g, gt, gy, nunits);
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
       float ms;
@@ -149,6 +149,10 @@ int main() {
   measure<4, 0>(t, y, g, gt, gy, ntiles, cus, bytes);
   measure<4, 1>(t, y, g, gt, gy, ntiles, cus, bytes);
   measure<8, 0>(t, y, g, gt, gy, ntiles, cus, bytes);
+  // the gradient stores write-through (sc1: the line leaves L2) instead of non-temporal
+  measure<1, 1, 16>(t, y, g, gt, gy, ntiles, cus, bytes);
+  measure<4, 0, 16>(t, y, g, gt, gy, ntiles, cus, bytes);
+  measure<1, 1, 0>(t, y, g, gt, gy, ntiles, cus, bytes);
   CHECK(hipFree(t));
   CHECK(hipFree(gt));
   CHECK(hipFree(y));
