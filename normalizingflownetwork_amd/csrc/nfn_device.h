@@ -111,6 +111,7 @@ struct ChainArgs {
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
   int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
+  int32_t load_aux;    // diagnostic (NFN_LOAD_AUX, diag builds): chain_wave1_kernel's row-load cache policy
   int32_t store_aux;   // diagnostic (NFN_STORE_AUX, diag builds): the forward kernels' log_prob store cache policy (store_out32)
   int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
   int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace fma in 8 independent chains (< 0)
@@ -1399,7 +1400,29 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       }
       ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
     } else {
+#ifdef NFN_DIAG
+      if (a.load_aux == 102)  // y-load policy study: nt instead of the default policy
+        ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 2));
+      else if (a.load_aux == 116)  // y-load policy study: sc1
+        ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 16));
+      else
+#endif
       ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+#ifdef NFN_DIAG
+      // load-policy study (NFN_LOAD_AUX: 16 = sc1, 18 = sc1 nt, 3 = sc0 nt; else nt)
+      if (a.load_aux == 16 || a.load_aux == 18 || a.load_aux == 3) {
+#pragma unroll
+        for (int k = 0; k < Q; ++k) {
+          if (a.load_aux == 16)
+            buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 16));
+          else if (a.load_aux == 18)
+            buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 18));
+          else
+            buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 3));
+        }
+        return;
+      }
+#endif
 #pragma unroll
       for (int k = 0; k < Q; ++k)
         buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
