@@ -1313,8 +1313,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-// The per-tile log_prob store of the streaming forward kernels (wave1, posterior_wave1,
-// group1).  Cache policy kOutAux = sc1 (aux bits 16: write-through, the line is dropped from
+// The per-tile log_prob (and, for the Chain bijector, z_K) stores of the streaming forward
+// kernels (wave1, posterior_wave1, group1).  Cache policy kOutAux = sc1 (aux bits 16: write-through, the line is dropped from
 // the XCD's L2) instead of non-temporal (2): in the bench harness the C2 stream with the
 // compile-time pair bodies runs 0.378-0.380 ms with sc1 stores against 0.389-0.391 with nt
 // (three boxes, profiles/r05/r05u / r05v / r05w_*), C3 -0.5 %, C5 unchanged; the memory-only
@@ -1439,7 +1439,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   auto flush = [&]() {
     store_out32(pend_v, pend_r, lane * 4, a);
     if constexpr (FWD)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pend_z), pend_rz, lane * 4, 0, kNT);
+      store_out32(pend_z, pend_rz, lane * 4, a);
   };
   issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
@@ -2233,7 +2233,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
 #pragma unroll
       for (int i = 0; i < DPL; ++i)
         if (FULL || j + G * i < a.d)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z[i]), rz, (sl * a.d + j + G * i) * 4, 0, kNT);
+          store_out32(z[i], rz, (sl * a.d + j + G * i) * 4, a);
     } else if (j == 0 && sl < nr) {
       acc += (double)lp;
       nfc += nonfinite1(lp);
