@@ -156,6 +156,11 @@ for s in $STEPS; do
           python3 "$ROOT/bench.py" $args --steps 3 --warmup 1 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       done ;;
     bijector) run bench_bijector 300 python bench.py --mode bijector --steps 30 --warmup 5 --cpu-seconds 6 ;;
+    r2) run bench_r2 200 python bench.py --config R2 --steps 50 --warmup 10 --no-cpu-baseline ;;
+    r10) run bench_r10 200 python bench.py --config R10 --steps 50 --warmup 10 --no-cpu-baseline ;;
+    grid) run bench_grid 200 python bench.py --mode grid --steps 30 --warmup 5 --no-cpu-baseline ;;
+    flows) run bench_flows 300 python bench.py --mode flows --steps 20 --warmup 5 --no-cpu-baseline ;;
+    dense_c3p) run bench_dense_c3p 300 python bench.py --mode dense --config C3P --steps 20 --warmup 5 --no-cpu-baseline ;;
     pairtests) run pairtests 300 python -u -m pytest tests/test_gpu_pairs.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     parity) run parity 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     sampleerr) run sampleerr 200 python tools/sample_err.py ;;
