@@ -236,6 +236,8 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   a.pace_rand = env_int("NFN_PACE_RAND", 0);
   a.store_aux = env_int("NFN_STORE_AUX", -1);
   a.load_aux = env_int("NFN_LOAD_AUX", -1);
+  a.early_issue = env_int("NFN_EARLY_ISSUE", 0);
+  a.split_issue = env_int("NFN_SPLIT_ISSUE", 0);
   a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // measured +1-2% (C2, C5); 2 = + static split
   {
     const int32_t rc = check_chain_args(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, P, y_mean, y_std, out_sum,

@@ -115,6 +115,8 @@ struct ChainArgs {
   int32_t store_aux;   // diagnostic (NFN_STORE_AUX, diag builds): the forward kernels' log_prob store cache policy (store_out32)
   int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
   int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace fma in 8 independent chains (< 0)
+  int32_t split_issue; // diagnostic (NFN_SPLIT_ISSUE, diag builds): launch selects chain_wave1_kernel<..., SPLIT = true>
+  int32_t early_issue; // diagnostic (NFN_EARLY_ISSUE, diag builds): chain_wave1_kernel issues the next tile before the hand-off's LDS wait
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
@@ -722,6 +724,22 @@ __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, 
     l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
   }
   return l2;
+}
+
+// n pairs of an alternating program from the block ending at `off` (advanced): the U = 1 body
+// of chain1_fast_hpairs, so two calls over [0, h) and [h, K / 2) plus the odd tail give its
+// values bitwise (chain_wave1_kernel<..., SPLIT>: the next tile's second half issues between).
+template <int IA, int IB, int ST = 1>
+__device__ __forceinline__ void hpairs_range(float& z, float& l2, const float* row, int& off, int n) {
+  constexpr int SA = IA == NFN_FLOW_AFFINE ? 2 : 3, SB = IB == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + SB;
+#pragma unroll 1
+  for (int p = 0; p < n; ++p) {
+    float pa[3], pb[3];
+    read3c<ST>(pa, row, off - SA);
+    read3c<ST>(pb, row, off - SP);
+    flow_pair1<IA, IB>(z, l2, pa, pb);
+    off -= SP;
+  }
 }
 
 // chain1_fast_pairs over TWO rows that share the program (two draws of one sample in the
@@ -1347,8 +1365,10 @@ __device__ __forceinline__ void store_out32(float v, __amdgpu_buffer_rsrc_t r, i
 // into the other of two LDS slots per wave while the chain reads the current one; no
 // register prefetch, no ds_write hand-off.  The next hand-off waits with an explicit
 // vmcnt(1) (hipcc does not order a ds_read behind an LDS-DMA).
-template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop, bool DMA = false>
+template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop, bool DMA = false, bool SPLIT = false>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
+  static_assert(!SPLIT || (FAST && !FWD && !DMA && CM >= kChainHPair && (CM - kChainHPair) / 9 == 1),
+                "SPLIT: the diagnostic split issue runs the U = 1 pair bodies of the log_prob form");
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
   constexpr int RSTEP = 64 / Q;  // rows per wave-instruction
@@ -1383,7 +1403,8 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   // waitcnt pass counts each hand-off's wait exactly.
   float4 buf[DMA ? 1 : Q];
   float ybuf;
-  auto issue = [&](int64_t tile) {
+  // part: 2 = the whole tile; SPLIT's halves 0 = y + the first Q / 2 row pieces, 1 = the rest
+  auto issue = [&](int64_t tile, int part = 2) {
     if (abl_tile >= 0) tile = abl_tile;
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
@@ -1401,31 +1422,38 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
     } else {
 #ifdef NFN_DIAG
-      if (a.load_aux == 102)  // y-load policy study: nt instead of the default policy
-        ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 2));
-      else if (a.load_aux == 116)  // y-load policy study: sc1
-        ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 16));
-      else
-#endif
-      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
-#ifdef NFN_DIAG
-      // load-policy study (NFN_LOAD_AUX: 16 = sc1, 18 = sc1 nt, 3 = sc0 nt; else nt)
-      if (a.load_aux == 16 || a.load_aux == 18 || a.load_aux == 3) {
-#pragma unroll
-        for (int k = 0; k < Q; ++k) {
-          if (a.load_aux == 16)
-            buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 16));
-          else if (a.load_aux == 18)
-            buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 18));
+      // load-policy study, one branch that returns (the default path below stays straight-line):
+      // NFN_LOAD_AUX 102 / 116 = y nt / sc1 (rows nt); 16 / 18 / 3 = rows sc1 / sc1 nt / sc0 nt
+      if constexpr (!SPLIT) {
+        const int la = a.load_aux;
+        if (la == 102 || la == 116 || la == 16 || la == 18 || la == 3) {
+          const int ya = la == 102 ? 2 : la == 116 ? 16 : 0, ta = la >= 100 ? kNT : la;
+          if (ya == 2)
+            ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 2));
+          else if (ya == 16)
+            ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 16));
           else
-            buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 3));
+            ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+#pragma unroll
+          for (int k = 0; k < Q; ++k) {
+            if (ta == 16)
+              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 16));
+            else if (ta == 18)
+              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 18));
+            else if (ta == 3)
+              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 3));
+            else
+              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+          }
+          return;
         }
-        return;
       }
 #endif
+      if (part != 1) ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
 #pragma unroll
       for (int k = 0; k < Q; ++k)
-        buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
+        if (part == 2 || (k < Q / 2) == (part == 0))
+          buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
     }
   };
 
@@ -1469,12 +1497,43 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       }
     }
     const float z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
-    wave_lds_sync();
-    issue(tile + ustep);
-    flush();
+#ifdef NFN_DIAG
+    if (SPLIT) {
+      wave_lds_sync();
+      issue(tile + ustep, 0);
+    } else if (a.early_issue) {  // the next tile's loads go out behind the ds_writes, before their wait
+      issue(tile + ustep);
+      flush();
+      wave_lds_sync();
+    } else
+#endif
+    {
+      wave_lds_sync();
+      issue(tile + ustep);
+      flush();
+    }
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     float lp;
-    if constexpr (FWD) {
+    if constexpr (SPLIT) {
+      // diagnostic: the next tile's second half issues after the first half of the pairs, so
+      // a wave holds ~half a tile in flight once the first half has landed
+      constexpr int c = CM - kChainHPair;
+      constexpr int IA = (c % 9) / 3, IB = c % 3;
+      const float* row = tl + lane * S;
+      float z = z0, l2 = 0.0f;
+      int off = a.P;
+      const int np = a.prog.K >> 1, h = np >> 1;
+      hpairs_range<IA, IB>(z, l2, row, off, h);
+      issue(tile + ustep, 1);
+      flush();
+      hpairs_range<IA, IB>(z, l2, row, off, np - h);
+      if (a.prog.K & 1) {
+        float pa[3];
+        read3c(pa, row, off - (IA == NFN_FLOW_AFFINE ? 2 : 3));
+        l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+      }
+      lp = base1_fast(z, row, a.trainable != 0) + l2 * kLn2 - corr;
+    } else if constexpr (FWD) {
       static_assert(FAST && PACKED, "the Chain bijector form uses the packed fast-math chain");
       float z = z0;
       lp = (a.prog.K > 0 ? chain1_fast_packed(z, tl + lane * S, a.prog.types[0], a.prog.K, a.P) : 0.0f) * kLn2;

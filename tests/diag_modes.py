@@ -65,6 +65,20 @@ def strategies():
         os.environ.pop("NFN_POST_SPLIT")
     np.testing.assert_allclose(out.cpu().numpy(), out1.cpu().numpy(), rtol=2e-6, atol=2e-6)
     res["post_split_vs_single"] = "allclose 2e-6"
+    # C2 shape on chain_wave1_kernel (ragged tail): the hand-off issue orders under study give
+    # the default order's values bitwise (the same pair bodies on the same rows)
+    B2 = (1 << 20) + 37
+    y2 = torch.randn((B2, 1), generator=gen, device="cuda")
+    t2 = torch.randn((B2, 32), generator=gen, device="cuda")
+    base, _ = ops.chain_log_prob(y2, t2, ft, 1, True)
+    for knob in ("NFN_SPLIT_ISSUE", "NFN_EARLY_ISSUE"):
+        os.environ[knob] = "1"
+        try:
+            got, _ = ops.chain_log_prob(y2, t2, ft, 1, True)
+        finally:
+            os.environ.pop(knob)
+        assert torch.equal(got, base), knob
+        res[knob.lower()] = "bitwise"
     res["library"] = os.path.basename(_lib.LIB_PATH)
     return res
 
