@@ -11,7 +11,11 @@ count) — the mean log-likelihood.
 One step = the fused chain kernel over the rank's batch (writes log_prob (B,)
 and per-workgroup fp64 partial sums) + the partials reduce + (N > 1) the
 all-reduce.  Inputs are synthetic N(0,1) float32 generated on the device and
-resident in HBM before the timed region.
+resident in HBM before the timed region.  The dominant kernel's duration (`roofline`) comes
+from HIP events that the step's launch records from its own dispatch (the library's
+nfn_set_launch_events hook, hipExtLaunchKernel): no marker packets sit between the timed
+steps, so the wall clock (`value`) carries no timing overhead (`--event-mode marker`: the
+older hipEventRecord pair around every step).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C5|C3P]
                   [--mode forward|grad|dense|dense_grad|bijector|flows [--flow-params views|separate|strided]]
@@ -25,6 +29,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -37,7 +42,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from normalizingflownetwork_amd import ops  # noqa: E402
+from normalizingflownetwork_amd import _lib, ops  # noqa: E402
 from normalizingflownetwork_amd.parallel import init_from_env  # noqa: E402
 
 C2_FLOWS = ("planar", "radial") * 5
@@ -297,6 +302,12 @@ def main():
                          "step; E > 1 keeps most of the events' ~4 us per step out of the wall clock, but "
                          "then a timed launch's interval includes the dispatch gap: +1 %% at C2, "
                          "profiles/r03/r03u_event_sampling_ab.log)")
+    ap.add_argument("--event-mode", default="auto", choices=["auto", "dispatch", "marker"],
+                    help="how the timed steps' kernel events are recorded: 'dispatch' arms "
+                         "nfn_set_launch_events so the step's first (dominant) launch records them from its own "
+                         "dispatch (hipExtLaunchKernel: no marker packets between steps); 'marker' records "
+                         "them with hipEventRecord around the whole step; 'auto' = dispatch for every mode "
+                         "whose step is one dominant launch, marker for --mode flows (ten launches)")
     ap.add_argument("--flow-params", default="views", choices=["views", "separate", "strided"],
                     help="--mode flows: the flows' parameters as views of the layer's one wide t (each step "
                          "first makes the blocks contiguous in one pass, nfn_split_blocks_f32, as the "
@@ -310,8 +321,6 @@ def main():
                          "communicator (nfn_allreduce_mean, stream-ordered; needs --backend nccl)")
     args = ap.parse_args()
     if args.diag:  # measurement tool only: the NFN_DIAG library reads NFN_* ablation / tuning knobs
-        from normalizingflownetwork_amd import _lib
-
         _lib.use_diagnostic_build()
     nfn_env = nfn_environment(allow_ablation=args.diag)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -398,6 +407,9 @@ def main():
 
         native = NativeComm()
 
+    ev_dispatch = args.event_mode == "dispatch" or (args.event_mode == "auto" and args.mode != "flows")
+    set_events = _lib.load().nfn_set_launch_events
+
     def step(ev0=None, ev1=None):
         if direct:
             i = nstep[0] % 2
@@ -405,10 +417,12 @@ def main():
             if works[i] is not None:
                 works[i].wait()  # stream-side wait: the slot's previous all-reduce is done
             launcher.bind_sum(reds[i])
-        if ev0 is not None:
+        if ev0 is not None and ev_dispatch:
+            set_events(ctypes.c_void_p(ev0.cuda_event), ctypes.c_void_p(ev1.cuda_event))
+        elif ev0 is not None:
             ev0.record(stream)
         launcher.launch(sh)
-        if ev1 is not None:
+        if ev1 is not None and not ev_dispatch:
             ev1.record(stream)
         if grad_mode or args.mode in ("bijector", "flows", "grid"):  # per-sample outputs stay on their rank
             return
@@ -475,12 +489,17 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
-    # the dominant kernel's duration: HIP events on its stream around the launches of the
-    # timed steps (every step by default: then the kernel times agree with rocprof's; the
-    # event pairs add ~4 us per step to the wall clock, which `value` keeps)
+    # the dominant kernel's duration: HIP events recorded by its own dispatch (default), or
+    # hipEventRecord markers on its stream around the launches of the timed steps (every step
+    # by default; the marker pairs add ~4 us per step to the wall clock, which `value` keeps)
     ev_every = max(1, args.event_every)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(0, args.steps, ev_every)]
+    if ev_dispatch:  # torch creates an event's HIP handle at its first record: create them now
+        for e0, e1 in evs:
+            e0.record(stream)
+            e1.record(stream)
+        torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
@@ -682,6 +701,7 @@ def main():
                 "kernel": kernel_name,
                 "kernel_ms": kern_ms,
                 "kernel_ms_launches": len(evs),
+                "kernel_events": "dispatch" if ev_dispatch else "marker",
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "traffic_source": traffic_src,
             },

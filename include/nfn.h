@@ -101,17 +101,27 @@ extern "C" {
 #define NFN_COMM_ID_BYTES 128
 
 /* Library version as MAJOR*10000 + MINOR*100 + PATCH.
+ *   203 (0.2.3): + nfn_set_launch_events (additive, measurement hook).
  *   202 (0.2.2): + nfn_flow_vjp_f32 (additive).
  *   201 (0.2.1): + nfn_split_blocks_f32 (additive; every 200 entry point unchanged).
  *   200 (0.2.0): out_sum is a device double[2] {sum, non-finite count} (was double[1]);
  *                the workspace needs no initialisation (its finishing ticket carries a
  *                per-call epoch).
  *   100 (0.1.0): first release. */
-#define NFN_ABI_VERSION 202
+#define NFN_ABI_VERSION 203
 int32_t nfn_version(void);
 
 /* Message of the last failing call on this thread ("" if none). */
 const char* nfn_last_error(void);
+
+/* Measurement hook (no reference counterpart: the reference has no device timing).  The
+ * NEXT kernel launch made on the calling thread records start_event / stop_event (hipEvent_t,
+ * created by the caller, e.g. torch.cuda.Event(enable_timing=True) after one record) from its
+ * own dispatch (hipExtLaunchKernel: the dispatch packet's start / end timestamps), then the
+ * hook clears; later launches of the same call go unrecorded.  Unlike hipEventRecord markers
+ * around the call, nothing is queued between consecutive launches.  (NULL, NULL) clears a
+ * pending pair.  Returns NFN_OK. */
+int32_t nfn_set_launch_events(void* start_event, void* stop_event);
 
 /* Transcendental implementation used by later launches in this process:
  * 0 = fast (gfx950 v_exp/v_log/v_rcp with stable rewrites; the default),

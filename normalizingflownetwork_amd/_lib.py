@@ -23,6 +23,7 @@ SIGNATURES = {
     "nfn_version": (_c_int32, []),
     "nfn_last_error": (ctypes.c_char_p, []),
     "nfn_set_math_mode": (_c_int32, [_c_int32]),
+    "nfn_set_launch_events": (_c_int32, [_vp, _vp]),
     "nfn_reduce_sum_f64": (_c_int32, [_vp, _c_int64, _vp, _vp]),
     "nfn_reduce_partials_f64": (_c_int32, [_vp, _vp, _vp]),
     "nfn_param_size": (_c_int32, [_c_int32, _c_int32]),
@@ -100,7 +101,7 @@ NFN_COMM_ID_BYTES = 128
 # include/nfn.h NFN_ABI_VERSION: the binding's argument conventions (out_sum double[2],
 # uninitialised workspaces) and its symbol table (nfn_split_blocks_f32 since 201,
 # nfn_flow_vjp_f32 since 202)
-ABI_VERSION = 202
+ABI_VERSION = 203
 
 _lib = None
 

@@ -11,6 +11,9 @@
 namespace nfn {
 
 thread_local std::string g_last_error;
+thread_local LaunchEvents g_launch_events;  // nfn_set_launch_events
+
+LaunchEvents& launch_events() { return g_launch_events; }
 
 int32_t set_error(int32_t code, const char* msg) {
   g_last_error = msg;
@@ -806,6 +809,12 @@ int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* strea
   if (!out || (n > 0 && !in)) return fail(NFN_E_NULLPTR, "in or out is NULL");
   launch_reduce_f64(in, n, out, reinterpret_cast<hipStream_t>(stream));
   return check_hip("reduce_f64_kernel launch");
+}
+
+int32_t nfn_set_launch_events(void* start_event, void* stop_event) {
+  g_launch_events.start = reinterpret_cast<hipEvent_t>(start_event);
+  g_launch_events.stop = reinterpret_cast<hipEvent_t>(stop_event);
+  return NFN_OK;
 }
 
 int32_t nfn_set_math_mode(int32_t mode) {

@@ -71,14 +71,14 @@ int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_co
     return set_error(NFN_E_NULLPTR, "nfn_allreduce_mean: NULL comm, local_sum or sum_count");
   if (local_count < 0) return set_error(NFN_E_SHAPE, "nfn_allreduce_mean: negative local_count");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  pack_sum_count_kernel<<<1, 1, 0, s>>>(local_sum, (double)local_count, sum_count);
+  nfn_launch((pack_sum_count_kernel), 1, 1, 0, s, local_sum, (double)local_count, sum_count);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NFN_E_HIP, hipGetErrorString(e));
   const ncclResult_t r = ncclAllReduce(sum_count, sum_count, 3, ncclFloat64, ncclSum,
                                        static_cast<ncclComm_t>(comm), s);
   if (r != ncclSuccess) return comm_fail(r, "ncclAllReduce");
   if (mean_out) {
-    finish_mean_kernel<<<1, 1, 0, s>>>(sum_count, mean_out);
+    nfn_launch((finish_mean_kernel), 1, 1, 0, s, sum_count, mean_out);
     e = hipGetLastError();
     if (e != hipSuccess) return set_error(NFN_E_HIP, hipGetErrorString(e));
   }

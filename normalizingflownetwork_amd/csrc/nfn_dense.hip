@@ -703,7 +703,7 @@ void launch_pdp(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const size_t lds = (size_t)(4 * (64 * da.h_lds_stride + 64 * da.c.lds_stride) + 16) * sizeof(float);
   const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
 }
 
 template <int DM>
@@ -725,7 +725,7 @@ void launch_pd1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
                                                                                 : posterior_dense1_kernel<QH, 4, CM>));
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
 }
 
 #ifndef NFN_DENSE_HP
@@ -749,7 +749,7 @@ void launch_pd(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const size_t lds = (size_t)(4 * (64 * da.h_lds_stride + 64 * da.c.lds_stride) + 16) * sizeof(float);
   const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
 }
 
 template <bool FAST>
@@ -799,7 +799,7 @@ void launch_d1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
                                                                            : chain_dense1_kernel<QH, 4, CM>));
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
 }
 
 #ifndef NFN_DENSE_HP
@@ -831,7 +831,7 @@ void launch_d(const DenseArgs& da, size_t lds, hipStream_t s, int64_t* grid_out)
   auto kfn = chain_dense_kernel<DM, FAST, NVH>;
   const int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
 }
 
 template <int DM, bool FAST>

@@ -535,7 +535,7 @@ int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
   const size_t lds = (size_t)4 * dense1_grad_wave_floats(g.da.c.P, 16 * MH + 4, g.da.c.prog.K) * sizeof(float);
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, max_parts));
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, g);
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, g);
   return grid;
 }
 
@@ -555,7 +555,7 @@ int64_t launch_dg(const DenseGradArgs& g, size_t lds, int64_t max_parts, hipStre
   auto kfn = chain_dense_grad_kernel<DM, FAST, MH, NN>;
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, max_parts));
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, g);
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, g);
   return grid;
 }
 
@@ -597,7 +597,7 @@ int64_t launch_dense_grad(bool fast, int dm, const DenseGradArgs& g, size_t lds,
 }
 
 void launch_sum_partials(const float* part, int64_t nparts, int n, float* gW, float* gb, int nW, hipStream_t s) {
-  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, s, part, (int)nparts, n,
+  nfn_launch(sum_partials_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, s, part, (int)nparts, n,
                      gW, gb, nW);
 }
 

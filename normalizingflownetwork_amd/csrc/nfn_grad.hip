@@ -464,7 +464,7 @@ bool launch_pc_q(const GradArgs& ga, hipStream_t s, int64_t* grid) {
   const size_t lds = (size_t)C * (64 * ga.c.lds_stride + ga.c.prog.K * 64) * sizeof(float);
   const int64_t nunits = (ga.c.ntiles + C - 1) / C;
   *grid = std::max<int64_t>(1, persistent_grid(k, 64 * (C + 1), lds, nunits));
-  k<<<dim3((unsigned)*grid), dim3(64 * (C + 1)), lds, s>>>(ga);
+  nfn_launch((k), dim3((unsigned)*grid), dim3(64 * (C + 1)), lds, s, ga);
   return true;
 }
 
@@ -478,7 +478,7 @@ bool launch_wave1_q(const GradArgs& ga, size_t lds_block, int wpb, hipStream_t s
     k = chain_grad_wave1_kernel<Q, kStaticProg>;
   const int T = 64 * wpb;
   *grid = std::max<int64_t>(1, persistent_grid(k, T, lds_block, (ga.c.ntiles + wpb - 1) / wpb));
-  k<<<dim3((unsigned)*grid), dim3(T), lds_block, s>>>(ga);
+  nfn_launch((k), dim3((unsigned)*grid), dim3(T), lds_block, s, ga);
   return true;
 }
 #endif  // NFN_DIAG
@@ -486,12 +486,12 @@ bool launch_wave1_q(const GradArgs& ga, size_t lds_block, int wpb, hipStream_t s
 template <bool FAST>
 void launch_grad_t(int dm, const GradArgs& ga, dim3 grid, size_t lds, hipStream_t s) {
   switch (dm) {
-    case 1: chain_grad_kernel<1, FAST><<<grid, 64, lds, s>>>(ga); break;
-    case 2: chain_grad_kernel<2, FAST><<<grid, 64, lds, s>>>(ga); break;
-    case 4: chain_grad_kernel<4, FAST><<<grid, 64, lds, s>>>(ga); break;
-    case 8: chain_grad_kernel<8, FAST><<<grid, 64, lds, s>>>(ga); break;
-    case 16: chain_grad_kernel<16, FAST><<<grid, 64, lds, s>>>(ga); break;
-    default: chain_grad_kernel<32, FAST><<<grid, 64, lds, s>>>(ga); break;
+    case 1: nfn_launch((chain_grad_kernel<1, FAST>), grid, 64, lds, s, ga); break;
+    case 2: nfn_launch((chain_grad_kernel<2, FAST>), grid, 64, lds, s, ga); break;
+    case 4: nfn_launch((chain_grad_kernel<4, FAST>), grid, 64, lds, s, ga); break;
+    case 8: nfn_launch((chain_grad_kernel<8, FAST>), grid, 64, lds, s, ga); break;
+    case 16: nfn_launch((chain_grad_kernel<16, FAST>), grid, 64, lds, s, ga); break;
+    default: nfn_launch((chain_grad_kernel<32, FAST>), grid, 64, lds, s, ga); break;
   }
 }
 
@@ -535,7 +535,7 @@ bool launch_wave_nv(const GradArgs& ga, size_t lds_block, int waves_per_block, h
   const int T = 64 * waves_per_block;
   const int64_t teams = persistent_grid(k, T, lds_block, (ga.c.ntiles + waves_per_block - 1) / waves_per_block);
   *grid = std::max<int64_t>(1, teams);
-  k<<<dim3((unsigned)*grid), dim3(T), lds_block, s>>>(ga);
+  nfn_launch((k), dim3((unsigned)*grid), dim3(T), lds_block, s, ga);
   return true;
 }
 
@@ -608,12 +608,12 @@ template <bool FAST>
 void launch_vjp_t(int dm, const FlowVjpArgs& v, dim3 grid, size_t lds, hipStream_t s) {
   const dim3 block(kMaxBlock);
   switch (dm) {
-    case 1: hipLaunchKernelGGL((flow_vjp_kernel<1, FAST>), grid, block, lds, s, v); break;
-    case 2: hipLaunchKernelGGL((flow_vjp_kernel<2, FAST>), grid, block, lds, s, v); break;
-    case 4: hipLaunchKernelGGL((flow_vjp_kernel<4, FAST>), grid, block, lds, s, v); break;
-    case 8: hipLaunchKernelGGL((flow_vjp_kernel<8, FAST>), grid, block, lds, s, v); break;
-    case 16: hipLaunchKernelGGL((flow_vjp_kernel<16, FAST>), grid, block, lds, s, v); break;
-    default: hipLaunchKernelGGL((flow_vjp_kernel<32, FAST>), grid, block, lds, s, v); break;
+    case 1: nfn_launch((flow_vjp_kernel<1, FAST>), grid, block, lds, s, v); break;
+    case 2: nfn_launch((flow_vjp_kernel<2, FAST>), grid, block, lds, s, v); break;
+    case 4: nfn_launch((flow_vjp_kernel<4, FAST>), grid, block, lds, s, v); break;
+    case 8: nfn_launch((flow_vjp_kernel<8, FAST>), grid, block, lds, s, v); break;
+    case 16: nfn_launch((flow_vjp_kernel<16, FAST>), grid, block, lds, s, v); break;
+    default: nfn_launch((flow_vjp_kernel<32, FAST>), grid, block, lds, s, v); break;
   }
 }
 

@@ -128,7 +128,7 @@ bool launch_wave2_q(const GradArgs& ga, hipStream_t s, int64_t* grid) {
   auto k = chain_grad_wave2_kernel<Q>;
   const size_t lds = (size_t)2 * (128 * ga.c.lds_stride + ga.c.prog.K * 128) * sizeof(float);
   *grid = std::max<int64_t>(1, persistent_grid(k, 128, lds, (ga.c.ntiles + 1) / 2));
-  k<<<dim3((unsigned)*grid), dim3(128), lds, s>>>(ga);
+  nfn_launch((k), dim3((unsigned)*grid), dim3(128), lds, s, ga);
   return true;
 }
 

@@ -450,7 +450,7 @@ void launch_gg1(const GradArgs& ga, hipStream_t s, int64_t* grid_out) {
   const int T = 64 * wpb;
   const int64_t grid = persistent_grid(kfn, T, lds_b, (ga.c.ntiles + wpb - 1) / wpb);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(T), lds_b, s, ga);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(T), lds_b, s, ga);
 }
 
 template <int G, int DPL, int NV>
@@ -473,7 +473,7 @@ void launch_gg(const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid_out)
   const int T = 64 * wpb;
   const int64_t grid = persistent_grid(kfn, T, lds_b, (ga.c.ntiles + wpb - 1) / wpb);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(T), lds_b, s, ga);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(T), lds_b, s, ga);
 }
 
 template <int G, int DPL>

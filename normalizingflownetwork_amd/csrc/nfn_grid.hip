@@ -154,15 +154,15 @@ void launch_grid_t(int dm, const GridArgs& ga, dim3 grid, dim3 block, size_t lds
     case 1:
       // NFN_GRID_PRE=0 (diag A/B): every grid value re-derives the parameter-only terms
       if (env_int("NFN_GRID_PRE", 1) != 0)
-        chain_grid_kernel<1, FAST><<<grid, block, lds, s>>>(ga);
+        nfn_launch((chain_grid_kernel<1, FAST>), grid, block, lds, s, ga);
       else
-        chain_grid_kernel<1, FAST, false><<<grid, block, lds, s>>>(ga);
+        nfn_launch((chain_grid_kernel<1, FAST, false>), grid, block, lds, s, ga);
       break;
-    case 2: chain_grid_kernel<2, FAST><<<grid, block, lds, s>>>(ga); break;
-    case 4: chain_grid_kernel<4, FAST><<<grid, block, lds, s>>>(ga); break;
-    case 8: chain_grid_kernel<8, FAST><<<grid, block, lds, s>>>(ga); break;
-    case 16: chain_grid_kernel<16, FAST><<<grid, block, lds, s>>>(ga); break;
-    default: chain_grid_kernel<32, FAST><<<grid, block, lds, s>>>(ga); break;
+    case 2: nfn_launch((chain_grid_kernel<2, FAST>), grid, block, lds, s, ga); break;
+    case 4: nfn_launch((chain_grid_kernel<4, FAST>), grid, block, lds, s, ga); break;
+    case 8: nfn_launch((chain_grid_kernel<8, FAST>), grid, block, lds, s, ga); break;
+    case 16: nfn_launch((chain_grid_kernel<16, FAST>), grid, block, lds, s, ga); break;
+    default: nfn_launch((chain_grid_kernel<32, FAST>), grid, block, lds, s, ga); break;
   }
 }
 

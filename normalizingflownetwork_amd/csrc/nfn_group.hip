@@ -26,13 +26,13 @@ void launch_g(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out) 
     if (env_int("NFN_WG_PER_CU", 0) <= 0) grid = std::min<int64_t>(grid, (int64_t)cu_count() * 2);
     grid = cap_grid(grid, a);
     *grid_out = grid;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+    nfn_launch(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
     return;
   }
   auto kfn = chain_group_kernel<G, DPL, kFast, NV, POST>;
   const int64_t grid = cap_grid(persistent_grid(kfn, kMaxBlock, lds, (a.ntiles + 3) / 4), a);  // 4 wave teams per WG
   *grid_out = grid;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
 }
 
 // float4 slots per thread: the exact count for the common widths (every slot is a
@@ -83,7 +83,7 @@ void launch_gf(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out)
                             : chain_group1_kernel<G, DPL, true, NV, false, true>;
   int64_t grid = std::min<int64_t>((a.ntiles + 3) / 4, (int64_t)cu_count() * 2);
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, a);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, a);
 }
 
 template <int G, int DPL>

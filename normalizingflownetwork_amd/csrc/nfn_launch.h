@@ -14,10 +14,33 @@
 
 #include "nfn_device.h"
 
+#include <hip/hip_ext.h>
+
 namespace nfn {
 
 // Record `msg` as this thread's nfn_last_error() and return `code` (nfn_api.hip).
 int32_t set_error(int32_t code, const char* msg);
+
+// nfn_set_launch_events: the calling thread's pending (start, stop) pair (nfn_api.hip).
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& launch_events();
+
+// Every kernel launch of the library: a plain launch, or — when the caller armed the
+// measurement hook — hipExtLaunchKernel with the pending events (the dispatch's own
+// timestamps), after which the hook clears.
+template <typename... Args, typename F = void (*)(Args...)>
+inline void nfn_launch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t s, Args... args) {
+  LaunchEvents& ev = launch_events();
+  if (ev.start != nullptr || ev.stop != nullptr) {
+    const LaunchEvents e = ev;
+    ev = LaunchEvents{};
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, e.start, e.stop, 0u, args...);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+  }
+}
 
 // Tuning / diagnostic knobs.  Only the NFN_DIAG build (libnfn_hip_diag.so, built for
 // tools/microbench.py) reads them from the environment; in the release library every

@@ -117,25 +117,25 @@ void launch_split_blocks(const SplitArgs& sa, hipStream_t s) {
   const int64_t span = split_dense(sa.rs, sa.W) ? std::max<int64_t>(sa.rs, sa.W) : sa.W;
   const size_t lds = (size_t)(R * span + 8) * sizeof(float);  // + the aligned span's up to 5 extra floats
   const int64_t nblk = (sa.B + R - 1) / R;
-  hipLaunchKernelGGL(split_blocks_kernel, dim3((unsigned)nblk), dim3(256), lds, s, sa);
+  nfn_launch(split_blocks_kernel, dim3((unsigned)nblk), dim3(256), lds, s, sa);
 }
 
 void launch_reduce_partials(const double* ws, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, s, ws, out);
+  nfn_launch(reduce_partials_kernel, dim3(1), dim3(256), 0, s, ws, out);
 }
 
 void launch_reduce_f64(const double* in, int64_t n, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_f64_kernel, dim3(1), dim3(1024), 0, s, in, n, out);
+  nfn_launch(reduce_f64_kernel, dim3(1), dim3(1024), 0, s, in, n, out);
 }
 
 void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, int64_t B, float* out, double* partials,
                             double* out_sum, uint32_t epoch, hipStream_t s) {
   const int64_t nblk = (B + kMaxBlock - 1) / kMaxBlock;
   if (fast)
-    hipLaunchKernelGGL(posterior_merge_kernel<true>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, parts, nsplit, S, B,
+    nfn_launch(posterior_merge_kernel<true>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, parts, nsplit, S, B,
                        out, partials, out_sum, epoch);
   else
-    hipLaunchKernelGGL(posterior_merge_kernel<false>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, parts, nsplit, S,
+    nfn_launch(posterior_merge_kernel<false>, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, parts, nsplit, S,
                        B, out, partials, out_sum, epoch);
 }
 

@@ -84,7 +84,7 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
     grid = std::min<int64_t>((units + teams - 1) / teams, (int64_t)cu_count() * wgs);
   grid = cap_grid(grid, a);
   *grid_out = grid;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }
 
 #if NFN_FAST
@@ -95,7 +95,7 @@ void launch_fw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out
   const int teams = kMaxBlock / 64;
   const int64_t grid = std::min<int64_t>((a.ntiles + teams - 1) / teams, (int64_t)cu_count() * (a.prog.K >= 4 ? 2 : 4));
   *grid_out = std::max<int64_t>(1, grid);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, a);
+  nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, a);
 }
 #endif
 
@@ -125,7 +125,7 @@ void launch_p(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gri
   const int teams = a.ownrow == 2 ? T / 64 : 1;
   const int64_t grid = cap_grid(persistent_grid(kfn, T, lds, (units + teams - 1) / teams), a);
   *grid_out = grid;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(T), lds, s, a);
 }
 
 template <int DM, bool POST>
@@ -180,11 +180,11 @@ void launch_pw1(const ChainArgs& a, size_t lds, hipStream_t s, int64_t* grid_out
 #ifdef NFN_DIAG
   // experiment: two draws per step (posterior_wave1x2_kernel), whole-tile units only
   if (env_int("NFN_POST_X2", 0) == 1 && a.nsplit == 1 && a.prog.K <= 16) {
-    hipLaunchKernelGGL(posterior_wave1x2_kernel<Q>, dim3((unsigned)grid), dim3(kMaxBlock), 2 * (lds - 16) + 16, s, a);
+    nfn_launch(posterior_wave1x2_kernel<Q>, dim3((unsigned)grid), dim3(kMaxBlock), 2 * (lds - 16) + 16, s, a);
     return;
   }
 #endif
-  hipLaunchKernelGGL(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, a);
 }
 #endif
 

@@ -170,12 +170,12 @@ __global__ void __launch_bounds__(kMaxBlock) chain_sample_kernel(SampleArgs sa) 
 template <bool FAST>
 void launch_sample_t(int dm, const SampleArgs& sa, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
   switch (dm) {
-    case 1: chain_sample_kernel<1, FAST><<<grid, block, lds, s>>>(sa); break;
-    case 2: chain_sample_kernel<2, FAST><<<grid, block, lds, s>>>(sa); break;
-    case 4: chain_sample_kernel<4, FAST><<<grid, block, lds, s>>>(sa); break;
-    case 8: chain_sample_kernel<8, FAST><<<grid, block, lds, s>>>(sa); break;
-    case 16: chain_sample_kernel<16, FAST><<<grid, block, lds, s>>>(sa); break;
-    default: chain_sample_kernel<32, FAST><<<grid, block, lds, s>>>(sa); break;
+    case 1: nfn_launch((chain_sample_kernel<1, FAST>), grid, block, lds, s, sa); break;
+    case 2: nfn_launch((chain_sample_kernel<2, FAST>), grid, block, lds, s, sa); break;
+    case 4: nfn_launch((chain_sample_kernel<4, FAST>), grid, block, lds, s, sa); break;
+    case 8: nfn_launch((chain_sample_kernel<8, FAST>), grid, block, lds, s, sa); break;
+    case 16: nfn_launch((chain_sample_kernel<16, FAST>), grid, block, lds, s, sa); break;
+    default: nfn_launch((chain_sample_kernel<32, FAST>), grid, block, lds, s, sa); break;
   }
 }
 

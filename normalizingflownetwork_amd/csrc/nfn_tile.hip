@@ -177,21 +177,21 @@ template <bool FAST>
 void launch_c_dm(int dm, const ChainArgs& a, dim3 grid, dim3 block, size_t lds, float* z_out, float* ldj_out,
                  hipStream_t s) {
   switch (dm) {
-    case 1: hipLaunchKernelGGL((chain_fwd_ldj_kernel<1, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
-    case 2: hipLaunchKernelGGL((chain_fwd_ldj_kernel<2, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
-    case 4: hipLaunchKernelGGL((chain_fwd_ldj_kernel<4, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
-    case 8: hipLaunchKernelGGL((chain_fwd_ldj_kernel<8, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
-    case 16: hipLaunchKernelGGL((chain_fwd_ldj_kernel<16, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
-    default: hipLaunchKernelGGL((chain_fwd_ldj_kernel<32, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 1: nfn_launch((chain_fwd_ldj_kernel<1, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 2: nfn_launch((chain_fwd_ldj_kernel<2, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 4: nfn_launch((chain_fwd_ldj_kernel<4, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 8: nfn_launch((chain_fwd_ldj_kernel<8, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    case 16: nfn_launch((chain_fwd_ldj_kernel<16, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
+    default: nfn_launch((chain_fwd_ldj_kernel<32, FAST>), grid, block, lds, s, a, z_out, ldj_out); break;
   }
 }
 
 template <int DM, bool FAST>
 void launch_t(const ChainArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t s, bool posterior) {
   if (posterior)
-    hipLaunchKernelGGL((posterior_lse_kernel<DM, FAST>), grid, block, lds, s, a);
+    nfn_launch((posterior_lse_kernel<DM, FAST>), grid, block, lds, s, a);
   else
-    hipLaunchKernelGGL((chain_logprob_kernel<DM, FAST>), grid, block, lds, s, a);
+    nfn_launch((chain_logprob_kernel<DM, FAST>), grid, block, lds, s, a);
 }
 
 template <bool FAST>
@@ -218,13 +218,13 @@ void launch_f(int32_t flow_id, const float* z, int64_t zs, const float* tk, int6
       const size_t lds = (size_t)kMaxBlock * ((ps | 1) + (d | 1)) * sizeof(float);
       auto kt = env_int("NFN_FLOW_STAGE", 1) != 0 ? flow_fwd_ldj_tile_kernel<DM, FAST, true>
                                                   : flow_fwd_ldj_tile_kernel<DM, FAST, false>;
-      kt<<<dim3((unsigned)nblk), dim3(kMaxBlock), lds, s>>>(flow_id, z, zs, tk, ts, B, d, ps, z_out, ldj_out);
+      nfn_launch((kt), dim3((unsigned)nblk), dim3(kMaxBlock), lds, s, flow_id, z, zs, tk, ts, B, d, ps, z_out, ldj_out);
       return;
     }
   }
   // NFN_FLOW_VARIANT=0 (diag A/B): the generic bijector code for d = 1 too
   auto k = env_int("NFN_FLOW_VARIANT", 1) == 0 ? flow_fwd_ldj_kernel<DM, FAST, 0> : flow_fwd_ldj_kernel<DM, FAST, 1>;
-  hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, flow_id, z, zs, tk, ts, B, d, z_out, ldj_out);
+  nfn_launch(k, dim3((unsigned)nblk), dim3(kMaxBlock), 0, s, flow_id, z, zs, tk, ts, B, d, z_out, ldj_out);
 }
 
 template <bool FAST>

@@ -45,12 +45,18 @@ def test_exported_symbols_are_c_linkage(native_lib):
 
 def test_version(native_lib):
     # 200: out_sum is double[2] and the workspace needs no initialisation; 201: + the
-    # additive nfn_split_blocks_f32; 202: + the additive nfn_flow_vjp_f32 (include/nfn.h)
+    # additive nfn_split_blocks_f32; 202: + the additive nfn_flow_vjp_f32; 203: + the
+    # measurement hook nfn_set_launch_events (include/nfn.h)
     from normalizingflownetwork_amd import _lib
 
-    assert native_lib.nfn_version() == _lib.ABI_VERSION == 202
+    assert native_lib.nfn_version() == _lib.ABI_VERSION == 203
     hdr = open(os.path.join(REPO, "include", "nfn.h")).read()
-    assert re.search(r"#define NFN_ABI_VERSION 202\b", hdr)
+    assert re.search(r"#define NFN_ABI_VERSION 203\b", hdr)
+
+
+def test_launch_events_hook_arms_and_clears(native_lib):
+    # host-only: arming and clearing the pending pair launches nothing (no GPU needed)
+    assert native_lib.nfn_set_launch_events(None, None) == 0
 
 
 def _ids(*names):
