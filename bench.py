@@ -297,11 +297,11 @@ def main():
                     help="--mode grid: grid values G (each evaluated under every one of the B parameter rows; "
                          "B defaults to 2^16, so G x B = 2^24 evals as at C2)")
     ap.add_argument("--hidden", type=int, default=16, help="--mode dense / dense_grad: hidden width H")
-    ap.add_argument("--event-every", type=int, default=1,
-                    help="time the dominant kernel with HIP events on every E-th timed step (default: every "
-                         "step; E > 1 keeps most of the events' ~4 us per step out of the wall clock, but "
-                         "then a timed launch's interval includes the dispatch gap: +1 %% at C2, "
-                         "profiles/r03/r03u_event_sampling_ab.log)")
+    ap.add_argument("--event-every", type=int, default=None,
+                    help="time the dominant kernel on every E-th timed step (default 4 with dispatch-recorded "
+                         "events: each timed launch still costs ~3 us of wall clock, but its interval is the "
+                         "kernel's own, profiles/r05/r05zi_*; 1 with markers, whose sampled intervals would "
+                         "include the dispatch gap: +1 %% at C2, profiles/r03/r03u_event_sampling_ab.log)")
     ap.add_argument("--event-mode", default="auto", choices=["auto", "dispatch", "marker"],
                     help="how the timed steps' kernel events are recorded: 'dispatch' arms "
                          "nfn_set_launch_events so the step's first (dominant) launch records them from its own "
@@ -388,7 +388,13 @@ def main():
             launcher = ops.GradLauncher(y, t, ft, d, True, g_out=g_up)
         else:
             launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
-    stream = torch.cuda.current_stream()
+    # the steps run on their own stream: HIP's legacy default stream synchronises with every
+    # other blocking stream on each launch, ~6 us per step between back-to-back kernels
+    # (tools/graph_gap.py, profiles/r05/r05zg*); inputs and launchers above were made on the
+    # default stream, so it is drained first
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sh = int(stream.cuda_stream)
     # (sum, non-finite) all-reduce buffers (the count is B per rank): a ring of two, so step i's all-reduce
     # (async, on the process group's stream) overlaps step i+1's chain kernel; a buffer
@@ -492,7 +498,7 @@ def main():
     # the dominant kernel's duration: HIP events recorded by its own dispatch (default), or
     # hipEventRecord markers on its stream around the launches of the timed steps (every step
     # by default; the marker pairs add ~4 us per step to the wall clock, which `value` keeps)
-    ev_every = max(1, args.event_every)
+    ev_every = max(1, args.event_every if args.event_every is not None else (4 if ev_dispatch else 1))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(0, args.steps, ev_every)]
     if ev_dispatch:  # torch creates an event's HIP handle at its first record: create them now

@@ -39,6 +39,7 @@ for s in $STEPS; do
     testsx) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     smoke) run smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 240 python bench.py --steps 50 --warmup 10 ;;
+    bench20) run bench20 240 python bench.py --gpus 1 --steps 20 --warmup 5 ;;  # the driver's command
     bench_nocpu) run bench_nocpu 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
     c3) run bench_c3 300 python bench.py --config C3 --steps 50 --warmup 10 --no-cpu-baseline ;;
     c5) run bench_c5 300 python bench.py --config C5 --steps 20 --warmup 5 --no-cpu-baseline ;;
