@@ -388,10 +388,9 @@ def main():
             launcher = ops.GradLauncher(y, t, ft, d, True, g_out=g_up)
         else:
             launcher = ops.ChainLauncher(y, t, ft, d, True, write_values=True, draws=S)
-    # the steps run on their own stream: HIP's legacy default stream synchronises with every
-    # other blocking stream on each launch, ~6 us per step between back-to-back kernels
-    # (tools/graph_gap.py, profiles/r05/r05zg*); inputs and launchers above were made on the
-    # default stream, so it is drained first
+    # the steps run on a stream of their own (back-to-back launches cost the same there as on
+    # the legacy default stream: tools/graph_gap.py, profiles/r05/r05zh); inputs and launchers
+    # above were made on the default stream, so it is drained first
     torch.cuda.synchronize()
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
