@@ -110,6 +110,76 @@ __global__ void __launch_bounds__(256) probe_kernel(const float* __restrict__ t,
   if (x[0] == 123.456f) sink[threadIdx.x] = x[1];
 }
 
+// G consecutive tiles per wave unit (the unit's G x 256 B of log_prob contiguous): the values
+// leave as one float4 store per lane per 4 tiles after the unit's last tile (lane l writes
+// samples 4l..4l+3 of a 4-tile group, transposed through LDS), policy POL.
+template <int G, int POL>
+__global__ void __launch_bounds__(256) group_kernel(const float* __restrict__ t, const float* __restrict__ y,
+                                                    float* __restrict__ out, int64_t ntiles, int work,
+                                                    float* __restrict__ sink) {
+  __shared__ float xl[4][G * 64];
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * 4 + wid, ws = (int64_t)gridDim.x * 4;
+  const int64_t nunits = ntiles / G;
+  f32x4 buf[8];
+  float yb = 0.f;
+  auto issue = [&](int64_t tile) {
+    const int64_t tc = tile < ntiles ? tile : 0;
+    const int nb = tile < ntiles ? 8192 : 0;
+    yb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(y + tc * 64, nb ? 256 : 0), lane * 4, 0, 0));
+    const auto r = rsrc(t + tc * 2048, nb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, k * 1024, 2));
+  };
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (float)(lane + j);
+  issue(w0 * G);
+  for (int64_t u = w0; u < nunits; u += ws) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      f32x4 s = buf[0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) s += buf[k];
+      const float v = s.x + s.y + s.z + s.w + yb;
+      issue(g + 1 < G ? u * G + g + 1 : (u + ws) * G);
+      busy(x, work);
+      xl[wid][g * 64 + lane] = v + x[g & 7];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const auto pr = rsrc(out + u * G * 64, G * 256);
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) {
+      const f32x4 o = *reinterpret_cast<const f32x4*>(&xl[wid][i * 256 + 4 * lane]);
+      __builtin_amdgcn_raw_buffer_store_b128(o, pr, lane * 16, i * 1024, POL);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (x[0] == 123.456f) sink[threadIdx.x] = x[1];
+}
+
+template <int G, int POL>
+float run_group(const float* t, const float* y, float* out, int64_t ntiles, int work, float* sink, int grid) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < 15; ++r) {
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL((group_kernel<G, POL>), dim3(grid), dim3(256), 0, 0, t, y, out, ntiles, work, sink);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return ts[ts.size() / 2];
+}
+
 template <int SPLIT, bool CONLY, bool HO = false>
 float run(const float* t, const float* y, float* out, int64_t ntiles, int work, float* sink, int grid) {
   hipEvent_t e0, e1;
@@ -148,6 +218,23 @@ int main() {
   CHECK(hipDeviceSynchronize());
   const double bytes = (double)tbytes + 8.0 * B;
   printf("C2-shaped stream (%.3f GB per launch) with `work` x 8 independent fma per tile\n", bytes / 1e9);
+  if (getenv("PROBE_GROUP")) {  // grouped log_prob stores, 8 waves per CU
+    const int grid = cus * 2;
+    for (int work : {0, 80}) {
+      const float a1 = run<0, false>(t, y, out, ntiles, work, sink, grid);
+      printf("wg/CU=2 work=%3d | per tile (b32 sc1) %.4f |", work, a1);
+      printf(" G=4 sc1 %.4f nt %.4f |", run_group<4, 16>(t, y, out, ntiles, work, sink, grid),
+             run_group<4, 2>(t, y, out, ntiles, work, sink, grid));
+      printf(" G=8 sc1 %.4f nt %.4f |", run_group<8, 16>(t, y, out, ntiles, work, sink, grid),
+             run_group<8, 2>(t, y, out, ntiles, work, sink, grid));
+      printf(" G=16 sc1 %.4f nt %.4f |", run_group<16, 16>(t, y, out, ntiles, work, sink, grid),
+             run_group<16, 2>(t, y, out, ntiles, work, sink, grid));
+      printf(" G=32 sc1 %.4f nt %.4f ms\n", run_group<32, 16>(t, y, out, ntiles, work, sink, grid),
+             run_group<32, 2>(t, y, out, ntiles, work, sink, grid));
+      fflush(stdout);
+    }
+    return 0;
+  }
   if (getenv("PROBE_HO")) {  // the hand-off form beside the register form, 8 waves per CU
     const int grid = cus * 2;
     for (int work : {0, 48, 64, 80, 96, 128}) {
