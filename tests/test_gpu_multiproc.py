@@ -54,6 +54,8 @@ def test_bench_nccl_step_path_one_rank(gpu, allreduce, config):
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["n_gpus"] == 1 and out["pg_world_size"] == 1 and np.isfinite(out["mean_log_prob"])
+    # the kernel interval comes from events the chain launch records itself (nfn_set_launch_events)
+    assert out["roofline"]["kernel_events"] == "dispatch" and out["roofline"]["kernel_ms"] > 0
     # the RCCL step path (the kernel finishing its sum straight into the all-reduce ring for
     # torch, the library communicator for native) gives exactly the plain N = 1 mean
     plain = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "2",
