@@ -633,8 +633,9 @@ def main():
             kernel_name = "chain_grad_wave_kernel" if d <= 2 else "chain_grad_group1_kernel"
             metric = f"log_prob backward evals/sec (whole node), {args.config}"
         elif args.mode == "dense_grad":
+            # dispatch-recorded events time the step's first launch; markers bracket both
             kernel_name = ("chain_dense1_grad_kernel" if d == 1 and H in (16, 32) else "chain_dense_grad_kernel") + \
-                " + sum_partials_kernel"
+                ("" if ev_dispatch else " + sum_partials_kernel")
             metric = f"Dense(H={H})->log_prob backward evals/sec (whole node), {args.config}"
         elif args.mode == "bijector":
             kernel_name = "chain_wave1_kernel (Chain bijector form)" if d == 1 else "chain_fwd_ldj_kernel"
