@@ -12,6 +12,9 @@ namespace nfn {
 
 thread_local std::string g_last_error;
 thread_local LaunchEvents g_launch_events;  // nfn_set_launch_events
+#ifdef NFN_DIAG
+unsigned long long* g_wave_times = nullptr;  // nfn_diag_wave_times
+#endif
 
 LaunchEvents& launch_events() { return g_launch_events; }
 
@@ -241,6 +244,10 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   a.load_aux = env_int("NFN_LOAD_AUX", -1);
   a.early_issue = env_int("NFN_EARLY_ISSUE", 0);
   a.split_issue = env_int("NFN_SPLIT_ISSUE", 0);
+  a.tile_rot = env_int("NFN_TILE_ROT", 0);
+#ifdef NFN_DIAG
+  a.wave_times = g_wave_times;
+#endif
   a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // measured +1-2% (C2, C5); 2 = + static split
   {
     const int32_t rc = check_chain_args(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, P, y_mean, y_std, out_sum,
@@ -810,6 +817,16 @@ int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* strea
   launch_reduce_f64(in, n, out, reinterpret_cast<hipStream_t>(stream));
   return check_hip("reduce_f64_kernel launch");
 }
+
+#ifdef NFN_DIAG
+// Diagnostic build only (not in include/nfn.h): later d = 1 wave-tile launches record each
+// wave's (start, end) wall_clock64() into buf[2 w], buf[2 w + 1] (the caller sizes buf for the
+// grid); NULL stops it.  tools/wave_tail.py.
+int32_t nfn_diag_wave_times(void* buf) {
+  g_wave_times = reinterpret_cast<unsigned long long*>(buf);
+  return NFN_OK;
+}
+#endif
 
 int32_t nfn_set_launch_events(void* start_event, void* stop_event) {
   g_launch_events.start = reinterpret_cast<hipEvent_t>(start_event);

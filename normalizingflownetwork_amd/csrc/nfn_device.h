@@ -116,6 +116,8 @@ struct ChainArgs {
   int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
   int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace fma in 8 independent chains (< 0)
   int32_t split_issue; // diagnostic (NFN_SPLIT_ISSUE, diag builds): launch selects chain_wave1_kernel<..., SPLIT = true>
+  unsigned long long* wave_times;  // diagnostic (nfn_diag_wave_times, diag builds): chain_wave1_kernel's per-wave (start, end) wall clock
+  int32_t tile_rot;    // chain_wave1_kernel: step k's tile slot for wave w is (w + k tile_rot) mod waves (0 = w)
   int32_t early_issue; // diagnostic (NFN_EARLY_ISSUE, diag builds): chain_wave1_kernel issues the next tile before the hand-off's LDS wait
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
@@ -1393,6 +1395,9 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   }
   // diagnostic (NFN_ABLATE_LOADS): every tile re-reads the wave's first tile
   const int64_t abl_tile = a.ablate_loads ? u0 : -1;
+#ifdef NFN_DIAG
+  const unsigned long long wt0 = a.wave_times ? wall_clock64() : 0ull;  // tail study (nfn_diag_wave_times)
+#endif
   // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
   const int yoff = lane * (int)a.y_bstride * 4;
   const int toff = (r0 * (int)rs + 4 * c4) * 4;
@@ -1469,9 +1474,18 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     if constexpr (FWD)
       store_out32(pend_z, pend_rz, lane * 4, a);
   };
+  // Step k covers tiles [k W, (k + 1) W) (W = ustep, the grid's waves); the wave takes slot
+  // (u0 + k rot) mod W of it, so with rot > 0 a workgroup's waves visit every part of each
+  // step's address range in turn instead of always the same one.
+  // (The slot advances incrementally: rot < W, no division.)
+  const int64_t rot = a.tile_rot % ustep;
   issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
-  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+  for (int64_t tile = u0, base = 0, slot = u0, tnext; tile < ntiles; tile = tnext) {
+    slot += rot;
+    if (slot >= ustep) slot -= ustep;
+    base += ustep;
+    tnext = base + slot;  // the next step's tile
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
@@ -1500,16 +1514,16 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
 #ifdef NFN_DIAG
     if (SPLIT) {
       wave_lds_sync();
-      issue(tile + ustep, 0);
+      issue(tnext, 0);
     } else if (a.early_issue) {  // the next tile's loads go out behind the ds_writes, before their wait
-      issue(tile + ustep);
+      issue(tnext);
       flush();
       wave_lds_sync();
     } else
 #endif
     {
       wave_lds_sync();
-      issue(tile + ustep);
+      issue(tnext);
       flush();
     }
     if (a.prio) __builtin_amdgcn_s_setprio(0);
@@ -1524,7 +1538,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
       int off = a.P;
       const int np = a.prog.K >> 1, h = np >> 1;
       hpairs_range<IA, IB>(z, l2, row, off, h);
-      issue(tile + ustep, 1);
+      issue(tnext, 1);
       flush();
       hpairs_range<IA, IB>(z, l2, row, off, np - h);
       if (a.prog.K & 1) {
@@ -1575,6 +1589,13 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     wave_lds_sync();  // this tile's LDS reads done before the next writes
   }
   flush();
+#ifdef NFN_DIAG
+  if (a.wave_times && lane == 0) {  // vector stores of this wave's (start, end)
+    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+    a.wave_times[2 * gw] = wt0;
+    a.wave_times[2 * gw + 1] = wall_clock64();
+  }
+#endif
   if (a.partials) {
     write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
