@@ -244,7 +244,11 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   a.load_aux = env_int("NFN_LOAD_AUX", -1);
   a.early_issue = env_int("NFN_EARLY_ISSUE", 0);
   a.split_issue = env_int("NFN_SPLIT_ISSUE", 0);
-  a.tile_rot = env_int("NFN_TILE_ROT", 0);
+  // Rotated tile slots (chain_wave1_kernel): each step a workgroup's waves take the slots one
+  // workgroup further on; C2 -1.4 % and R10 -1.3 % against the plain walk in the bench harness
+  // on two boxes (profiles/r05/r05zn, r05zq; two workgroups' shift gains nothing).
+  a.tile_rot = env_int("NFN_TILE_ROT", 4);
+  a.tile_rot_g = env_int("NFN_TILE_ROT_G", 0);
 #ifdef NFN_DIAG
   a.wave_times = g_wave_times;
 #endif

@@ -118,6 +118,7 @@ struct ChainArgs {
   int32_t split_issue; // diagnostic (NFN_SPLIT_ISSUE, diag builds): launch selects chain_wave1_kernel<..., SPLIT = true>
   unsigned long long* wave_times;  // diagnostic (nfn_diag_wave_times, diag builds): chain_wave1_kernel's per-wave (start, end) wall clock
   int32_t tile_rot;    // chain_wave1_kernel: step k's tile slot for wave w is (w + k tile_rot) mod waves (0 = w)
+  int32_t tile_rot_g;  // the same for chain_group1_kernel
   int32_t early_issue; // diagnostic (NFN_EARLY_ISSUE, diag builds): chain_wave1_kernel issues the next tile before the hand-off's LDS wait
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
@@ -2289,11 +2290,17 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   int nfc = 0;  // non-finite log_prob values
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
   float pend_v = 0.0f;
+  // rotated tile slots as in chain_wave1_kernel (a.tile_rot_g)
+  const int64_t rot = a.tile_rot_g % ustep;
   issue(u0);
   // an (empty) store behind the first prefetch too: every path into the loop then
   // ends [loads][store] and the hand-off waits with vmcnt(1), not vmcnt(0)
   store_out32(pend_v, pend_r, lane * 4, a);
-  for (int64_t tile = u0; tile < a.ntiles; tile += ustep) {
+  for (int64_t tile = u0, base = 0, slot = u0, tnext; tile < a.ntiles; tile = tnext) {
+    slot += rot;
+    if (slot >= ustep) slot -= ustep;
+    base += ustep;
+    tnext = base + slot;
     const int64_t b0 = tile * R;
     const int64_t nr = max((int64_t)0, min((int64_t)R, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(2);
@@ -2303,7 +2310,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
 #pragma unroll
     for (int i = 0; i < DPL; ++i) z[i] = norm ? f_div<FAST>(ybuf[i] - ymean[i], yrstd[i]) : ybuf[i];
     wave_lds_sync();
-    issue(tile + ustep);
+    issue(tnext);
     store_out32(pend_v, pend_r, lane * 4, a);
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     const float lp = eval_chain_gd<G, DPL, FAST, FULL, FWD>(z, tl + sl * S, a, j) - corr;

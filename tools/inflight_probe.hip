@@ -180,6 +180,100 @@ float run_group(const float* t, const float* y, float* out, int64_t ntiles, int 
   return ts[ts.size() / 2];
 }
 
+// Dynamic tail: steps k < Ks as the static walk, then the last D steps' tiles handed out C at a
+// time by one agent-scope fetch-add on a counter (zeroed before the launch), each grab issued
+// one chunk ahead of its use.
+template <int C, int NCTR = 1>
+__global__ void __launch_bounds__(256) dyn_kernel(const float* __restrict__ t, const float* __restrict__ y,
+                                                  float* __restrict__ out, int64_t ntiles, int work, int dsteps,
+                                                  unsigned long long* __restrict__ ctr, float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t w0 = (int64_t)blockIdx.x * 4 + wid, ws = (int64_t)gridDim.x * 4;
+  const int64_t ks = max((int64_t)1, ntiles / ws - dsteps), pool0 = ks * ws;
+  const int64_t nchunks = (ntiles - pool0 + C - 1) / C;
+  const int q = (int)(w0 % NCTR);
+  ctr += 16 * q;  // 128 B apart
+  f32x4 buf[8];
+  float yb = 0.f;
+  auto issue = [&](int64_t tile) {
+    const int64_t tc = tile < ntiles ? tile : 0;
+    const int nb = tile < ntiles ? 8192 : 0;
+    yb = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(y + tc * 64, nb ? 256 : 0), lane * 4, 0, 0));
+    const auto r = rsrc(t + tc * 2048, nb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      buf[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, k * 1024, 2));
+  };
+  unsigned long long fut = 0;
+  auto grab = [&]() {
+    if (lane == 0) fut = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (float)(lane + j);
+  int64_t knext = 1, cpos = 0, cleft = 0;
+  bool more = true;
+  if (ks == 1) grab();
+  issue(w0);
+  for (int64_t tile = w0, tnext; tile < ntiles; tile = tnext) {
+    f32x4 s = buf[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) s += buf[k];
+    const float v = s.x + s.y + s.z + s.w + yb;
+    if (knext < ks) {
+      tnext = knext * ws + w0;
+      if (++knext == ks) grab();
+    } else if (cleft > 0) {
+      tnext = cpos++;
+      --cleft;
+    } else if (more) {
+      const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane((unsigned)fut) * NCTR + q;
+      if (c < nchunks) {
+        cpos = pool0 + c * C;
+        cleft = min((int64_t)C, ntiles - cpos);
+        tnext = cpos++;
+        --cleft;
+        grab();
+      } else {
+        more = false;
+        tnext = ntiles;
+      }
+    } else {
+      tnext = ntiles;
+    }
+    issue(tnext);
+    busy(x, work);
+    float o = v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o += x[j];
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rsrc(out + tile * 64, 256), lane * 4, 0, 16);
+  }
+  if (x[0] == 123.456f) sink[threadIdx.x] = x[1];
+}
+
+template <int C, int NCTR = 1>
+float run_dyn(const float* t, const float* y, float* out, int64_t ntiles, int work, int dsteps,
+              unsigned long long* ctr, float* sink, int grid) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  std::vector<float> ts;
+  for (int r = 0; r < 15; ++r) {
+    CHECK(hipMemsetAsync(ctr, 0, 16 * 8 * NCTR, 0));
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL((dyn_kernel<C, NCTR>), dim3(grid), dim3(256), 0, 0, t, y, out, ntiles, work, dsteps, ctr, sink);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return ts[ts.size() / 2];
+}
+
 template <int SPLIT, bool CONLY, bool HO = false>
 float run(const float* t, const float* y, float* out, int64_t ntiles, int work, float* sink, int grid) {
   hipEvent_t e0, e1;
@@ -218,6 +312,26 @@ int main() {
   CHECK(hipDeviceSynchronize());
   const double bytes = (double)tbytes + 8.0 * B;
   printf("C2-shaped stream (%.3f GB per launch) with `work` x 8 independent fma per tile\n", bytes / 1e9);
+  if (getenv("PROBE_DYN")) {  // dynamic tail, 8 waves per CU, at the C2 chain's VALU time
+    const int grid = cus * 2;
+    unsigned long long* ctr;
+    CHECK(hipMalloc(&ctr, 16 * 8 * 8));
+    const int work = 80;
+    for (int rep = 0; rep < 2; ++rep) {
+      printf("work=%d static %.4f | D=4: C=4 %.4f C=8 %.4f C=16 %.4f, C=4 x8 ctr %.4f, C=8 x8 ctr %.4f |", work,
+             run_dyn<4>(t, y, out, ntiles, work, 0, ctr, sink, grid),
+             run_dyn<4>(t, y, out, ntiles, work, 4, ctr, sink, grid), run_dyn<8>(t, y, out, ntiles, work, 4, ctr, sink, grid),
+             run_dyn<16>(t, y, out, ntiles, work, 4, ctr, sink, grid),
+             run_dyn<4, 8>(t, y, out, ntiles, work, 4, ctr, sink, grid), run_dyn<8, 8>(t, y, out, ntiles, work, 4, ctr, sink, grid));
+      printf(" D=8: C=8 %.4f C=16 %.4f, C=4 x8 ctr %.4f, C=8 x8 ctr %.4f | D=16: C=8 x8 ctr %.4f C=16 x8 %.4f | D=2 C=4 %.4f ms\n",
+             run_dyn<8>(t, y, out, ntiles, work, 8, ctr, sink, grid), run_dyn<16>(t, y, out, ntiles, work, 8, ctr, sink, grid),
+             run_dyn<4, 8>(t, y, out, ntiles, work, 8, ctr, sink, grid), run_dyn<8, 8>(t, y, out, ntiles, work, 8, ctr, sink, grid),
+             run_dyn<8, 8>(t, y, out, ntiles, work, 16, ctr, sink, grid), run_dyn<16, 8>(t, y, out, ntiles, work, 16, ctr, sink, grid),
+             run_dyn<4>(t, y, out, ntiles, work, 2, ctr, sink, grid));
+      fflush(stdout);
+    }
+    return 0;
+  }
   if (getenv("PROBE_GROUP")) {  // grouped log_prob stores, 8 waves per CU
     const int grid = cus * 2;
     for (int work : {0, 80}) {
