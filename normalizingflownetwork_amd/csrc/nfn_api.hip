@@ -249,6 +249,7 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   // on two boxes (profiles/r05/r05zn, r05zq; two workgroups' shift gains nothing).
   a.tile_rot = env_int("NFN_TILE_ROT", 4);
   a.tile_rot_g = env_int("NFN_TILE_ROT_G", 0);
+  a.xcd_skew = env_int("NFN_XCD_SKEW", 0);
 #ifdef NFN_DIAG
   a.wave_times = g_wave_times;
 #endif

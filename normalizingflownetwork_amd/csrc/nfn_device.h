@@ -119,6 +119,7 @@ struct ChainArgs {
   unsigned long long* wave_times;  // diagnostic (nfn_diag_wave_times, diag builds): chain_wave1_kernel's per-wave (start, end) wall clock
   int32_t tile_rot;    // chain_wave1_kernel: step k's tile slot for wave w is (w + k tile_rot) mod waves (0 = w)
   int32_t tile_rot_g;  // the same for chain_group1_kernel
+  int32_t xcd_skew;    // chain_wave1_kernel: the last xcd_skew steps split 3 : 1 between even- and odd-XCD waves (0 = evenly)
   int32_t early_issue; // diagnostic (NFN_EARLY_ISSUE, diag builds): chain_wave1_kernel issues the next tile before the hand-off's LDS wait
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
@@ -1480,13 +1481,33 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   // step's address range in turn instead of always the same one.
   // (The slot advances incrementally: rot < W, no division.)
   const int64_t rot = a.tile_rot % ustep;
+  // XCD skew (a.xcd_skew = L > 0, even): the last L steps' L W tiles are not split evenly but
+  // 3 : 1 between the waves of even- and odd-numbered XCDs (workgroup b runs on XCD b mod 8),
+  // which finish their equal shares ~4 % apart (tools/wave_tail.py): an even-XCD wave takes 3L/2
+  // tiles of that block, an odd-XCD wave L/2.  Whole steps only (ntiles a multiple of W).
+  int64_t kf = INT64_MAX, soff = 0, scnt = 0;
+  const int64_t half = ustep >> 1;
+  if (a.xcd_skew > 0 && (a.xcd_skew & 1) == 0 && (gridDim.x & 7) == 0 && ntiles % ustep == 0 &&
+      ntiles / ustep > a.xcd_skew) {
+    const int L = a.xcd_skew;
+    const int b = blockIdx.x, x = b & 7, nwb = blockDim.x >> 6;
+    const int64_t rank = ((int64_t)(b >> 3) * 4 + (x >> 1)) * nwb + wid;  // among the even (odd) XCDs' waves
+    kf = ntiles / ustep - L;
+    scnt = (x & 1) ? L / 2 : 3 * L / 2;
+    soff = kf * ustep + ((x & 1) ? 3 * (int64_t)L * half / 2 : 0) + rank;
+  }
   issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
-  for (int64_t tile = u0, base = 0, slot = u0, tnext; tile < ntiles; tile = tnext) {
-    slot += rot;
-    if (slot >= ustep) slot -= ustep;
-    base += ustep;
-    tnext = base + slot;  // the next step's tile
+  for (int64_t tile = u0, base = 0, slot = u0, step = 0, tnext; tile < ntiles; tile = tnext, ++step) {
+    if (step + 1 < kf) {
+      slot += rot;
+      if (slot >= ustep) slot -= ustep;
+      base += ustep;
+      tnext = base + slot;  // the next step's tile
+    } else {
+      const int64_t m = step + 1 - kf;  // the next tile's place in this wave's share of the skewed block
+      tnext = m < scnt ? soff + m * half : ntiles;
+    }
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority

@@ -71,14 +71,25 @@ def strategies():
     y2 = torch.randn((B2, 1), generator=gen, device="cuda")
     t2 = torch.randn((B2, 32), generator=gen, device="cuda")
     base, _ = ops.chain_log_prob(y2, t2, ft, 1, True)
-    for knob in ("NFN_SPLIT_ISSUE", "NFN_EARLY_ISSUE"):
-        os.environ[knob] = "1"
+    for knob in ("NFN_SPLIT_ISSUE", "NFN_EARLY_ISSUE", "NFN_XCD_SKEW"):
+        os.environ[knob] = "6" if knob == "NFN_XCD_SKEW" else "1"
         try:
             got, _ = ops.chain_log_prob(y2, t2, ft, 1, True)
         finally:
             os.environ.pop(knob)
         assert torch.equal(got, base), knob
         res[knob.lower()] = "bitwise"
+    # the XCD-skewed last steps need whole steps: B = 2^20 (8 steps of the 2048-wave grid)
+    y3, t3 = y2[: 1 << 20], t2[: 1 << 20]
+    base3, s3 = ops.chain_log_prob(y3, t3, ft, 1, True, want_sum=True)
+    os.environ["NFN_XCD_SKEW"] = "6"
+    try:
+        got3, g3 = ops.chain_log_prob(y3, t3, ft, 1, True, want_sum=True)
+    finally:
+        os.environ.pop("NFN_XCD_SKEW")
+    assert torch.equal(got3, base3), "NFN_XCD_SKEW whole steps"
+    assert abs(float(g3.item()) - float(s3.item())) <= 1e-12 * abs(float(s3.item()))
+    res["nfn_xcd_skew_whole_steps"] = "bitwise"
     res["library"] = os.path.basename(_lib.LIB_PATH)
     return res
 

@@ -44,7 +44,8 @@ def test_diag_strategies_bitwise_equal(gpu):
     assert os.path.exists(build.DIAG_OUT), "libnfn_hip_diag.so is built by __graft_entry__.build()"
     res = _run("strategies")
     assert res["library"] == "libnfn_hip_diag.so"
-    assert all(res[m] == "bitwise" for m in ("coop", "wave", "ownrow", "tile", "nfn_split_issue", "nfn_early_issue"))
+    assert all(res[m] == "bitwise" for m in ("coop", "wave", "ownrow", "tile", "nfn_split_issue", "nfn_early_issue", "nfn_xcd_skew",
+                                        "nfn_xcd_skew_whole_steps"))
 
 
 def test_diag_grad_stream_bitwise_equal(gpu):
