@@ -463,6 +463,7 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   a.prio = env_int("NFN_PRIO", 1) == 1 ? 1 : 0;
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
   a.zonly = env_int("NFN_GRAD_ZONLY", 1) != 0 ? 1 : 0;
+  a.tile_rot = env_int("NFN_TILE_ROT_B", 0);  // chain_grad_wave_kernel's rotated tile slots (A/B knob)
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int Q = P >> 2;
   const int dm = dm_for(d);

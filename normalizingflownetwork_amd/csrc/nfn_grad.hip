@@ -129,10 +129,15 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
     }
   };
 
-  int64_t tile = u0;
   const int64_t ntiles = a.ntiles;
-  if (tile < ntiles) issue(tile);
-  for (; tile < ntiles; tile += ustep) {
+  // rotated tile slots (a.tile_rot: chain_wave1_kernel's walk; 0 = the plain grid stride)
+  const int64_t rot = a.tile_rot % ustep;
+  if (u0 < ntiles) issue(u0);
+  for (int64_t tile = u0, base = 0, slot = u0, tnext; tile < ntiles; tile = tnext) {
+    slot += rot;
+    if (slot >= ustep) slot -= ustep;
+    base += ustep;
+    tnext = base + slot;
     const int64_t b0 = tile * 64;
     const int nr = (int)min((int64_t)64, a.B - b0);
     if (a.prio) __builtin_amdgcn_s_setprio(2);
@@ -158,7 +163,7 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
     }
     const float gl = gbuf;
     wave_lds_sync();
-    if (tile + ustep < ntiles) issue(tile + ustep);
+    if (tnext < ntiles) issue(tnext);
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     if (lane < nr) {
       const int64_t b = b0 + lane;
