@@ -38,7 +38,6 @@ UNITS = [
     ("tile", "nfn_tile.hip", []),
     ("misc", "nfn_misc.hip", []),
     ("grad", "nfn_grad.hip", []),
-    ("grad2", "nfn_grad2.hip", ["-fno-slp-vectorize"]),  # diag A/B only (empty in the release library)
     ("grad_group_fast", "nfn_grad_group.hip", ["-DNFN_FAST=1"]),
     ("grad_group_precise", "nfn_grad_group.hip", ["-DNFN_FAST=0"]),
     ("grid", "nfn_grid.hip", []),

@@ -12,9 +12,6 @@ namespace nfn {
 
 thread_local std::string g_last_error;
 thread_local LaunchEvents g_launch_events;  // nfn_set_launch_events
-#ifdef NFN_DIAG
-unsigned long long* g_wave_times = nullptr;  // nfn_diag_wave_times
-#endif
 
 LaunchEvents& launch_events() { return g_launch_events; }
 
@@ -220,6 +217,31 @@ int32_t check_chain_args(const float* y, int64_t y_bstride, const float* t, int6
   return NFN_OK;
 }
 
+// The forward streaming policy of the release library — measured defaults:
+//  * t rows and log_prob are streamed once: non-temporal loads and stores (nt, nt_store);
+//  * rotated tile slots in chain_wave1_kernel: each step a workgroup's waves take the slots
+//    one workgroup further on; C2 -1.4 % and R10 -1.3 % against the plain walk in the bench
+//    harness on two boxes (profiles/r05/r05zn, r05zq; two workgroups' shift gains nothing);
+//  * wave priority raised around the tile hand-off (+1-2 % on C2, C5).
+// Only the diagnostic build (libnfn_hip_diag.so) reads NFN_* overrides for A/B studies.
+constexpr int kTileRot = 4;
+void forward_stream_policy(ChainArgs& a) {
+  a.nt = 1;
+  a.nt_store = 1;
+  a.tile_rot = kTileRot;
+  a.prio = 1;
+#ifdef NFN_DIAG
+  // NFN_ABLATE_FLOWS=1: stream the same parameter rows but skip the flow math (memory only)
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
+  a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;
+  a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
+  a.tile_rot = std::max(0, env_int("NFN_TILE_ROT", kTileRot));  // >= 0: the kernel's slot walk only wraps upward
+  a.tile_rot_g = std::max(0, env_int("NFN_TILE_ROT_G", 0));
+  a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // 2 = + static split
+#endif
+}
+
 // One launch over B samples.  A chunk of a longer batch (chunk_cap > 0) writes its
 // partial pairs after the earlier chunks' (from slot pair_base, at most chunk_cap of
 // them); only the last chunk finishes out_sum, over every chunk's pairs.
@@ -232,28 +254,7 @@ int32_t run_chain_launch(const float* y, int64_t y_bstride, const float* t, int6
   memset(&a, 0, sizeof(a));
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
   if (P < 0) return P;
-  // Diagnostic only (NFN_ABLATE_FLOWS=1): stream the same parameter rows but skip
-  // the flow math, to measure the memory path of the kernel structure alone.
-  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // NFN_DIAG builds only (env_int)
-  a.nt = env_int("NFN_NT_LOADS", 1) == 1 ? 1 : 0;        // t is streamed once: non-temporal
-  a.nt_store = env_int("NFN_NT_STORES", 1) == 1 ? 1 : 0;  // log_prob is written once: non-temporal
-  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
-  a.pace = env_int("NFN_PACE", 0);
-  a.pace_rand = env_int("NFN_PACE_RAND", 0);
-  a.store_aux = env_int("NFN_STORE_AUX", -1);
-  a.load_aux = env_int("NFN_LOAD_AUX", -1);
-  a.early_issue = env_int("NFN_EARLY_ISSUE", 0);
-  a.split_issue = env_int("NFN_SPLIT_ISSUE", 0);
-  // Rotated tile slots (chain_wave1_kernel): each step a workgroup's waves take the slots one
-  // workgroup further on; C2 -1.4 % and R10 -1.3 % against the plain walk in the bench harness
-  // on two boxes (profiles/r05/r05zn, r05zq; two workgroups' shift gains nothing).
-  a.tile_rot = env_int("NFN_TILE_ROT", 4);
-  a.tile_rot_g = env_int("NFN_TILE_ROT_G", 0);
-  a.xcd_skew = env_int("NFN_XCD_SKEW", 0);
-#ifdef NFN_DIAG
-  a.wave_times = g_wave_times;
-#endif
-  a.prio = std::min(std::max(env_int("NFN_PRIO", 1), 0), 2);  // measured +1-2% (C2, C5); 2 = + static split
+  forward_stream_policy(a);
   {
     const int32_t rc = check_chain_args(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, P, y_mean, y_std, out_sum,
                                         workspace, posterior);
@@ -384,6 +385,7 @@ int32_t run_chain(const float* y, int64_t y_bstride, const float* t, int64_t t_d
                   const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
                   void* stream, bool posterior) {
   g_last_error.clear();
+  const HookScope hook_scope;
   const int64_t chunk = posterior ? 0 : chain_chunk_rows();
   if (chunk <= 0 || B <= chunk || !y || (t == nullptr && t_rowstride != 0))
     return run_chain_launch(y, y_bstride, t, t_drawstride, t_rowstride, S, B, d, flow_ids, K, trainable_base, y_mean,
@@ -415,6 +417,7 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
                  const float* y_std, const float* g_out, float* out_logp, float* grad_t, int64_t gt_rowstride,
                  float* grad_y, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   GradArgs ga;
   memset(&ga, 0, sizeof(ga));
   ChainArgs& a = ga.c;
@@ -458,12 +461,17 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
   ga.gt_rowstride = grad_t ? gt_rowstride : 0;
   ga.gt_vec4 = ((P & 3) == 0) && ((gt_rowstride & 3) == 0) && ((reinterpret_cast<uintptr_t>(grad_t) & 15) == 0);
   ga.rows = R;
-  // diagnostics (microbenchmarks): memory-only / compute-only timing
+  // the backward's release policy: hand-off priority, z-only forward recompute when no
+  // log_prob is wanted; the diagnostic build's overrides (memory-only / compute-only timing)
+  a.prio = 1;
+  a.zonly = 1;
+#ifdef NFN_DIAG
   if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;
   a.prio = env_int("NFN_PRIO", 1) == 1 ? 1 : 0;
   a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;
   a.zonly = env_int("NFN_GRAD_ZONLY", 1) != 0 ? 1 : 0;
-  a.tile_rot = env_int("NFN_TILE_ROT_B", 0);  // chain_grad_wave_kernel's rotated tile slots (A/B knob)
+  a.tile_rot_b = std::max(0, env_int("NFN_TILE_ROT_B", 0));  // chain_grad_wave_kernel's rotated slots (A/B)
+#endif
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int Q = P >> 2;
   const int dm = dm_for(d);
@@ -487,18 +495,6 @@ int32_t run_grad(const float* y, int64_t y_bstride, const float* t, int64_t t_ro
     }
     a.lds_stride = S;
   }
-#ifdef NFN_DIAG
-  // diagnostic A/B (NFN_GRAD_WAVE2=1; measured and not adopted, DESIGN.md "C2 backward"):
-  // d = 1, fast math, P = 8, 16 or 32, two samples per lane over 128-row wave tiles
-  const size_t slot2 = (size_t)(128 * S + a.prog.K * 128) * sizeof(float);
-  if (wave_ok && use_fast_math() && d == 1 && Q <= 8 && slot2 * 2 <= (size_t)80 * 1024 &&
-      env_int("NFN_GRAD_WAVE2", 0) == 1) {
-    GradArgs g2 = ga;  // a local copy: a false return leaves the caller's tiling untouched
-    g2.c.ntiles = (B + 127) / 128;
-    int64_t grid = 0;
-    if (launch_grad_wave2(Q, g2, s, &grid)) return check_hip("chain_grad_wave2_kernel launch");
-  }
-#endif
   if (wave_ok) {
     a.ntiles = (B + 63) / 64;
     // two waves per workgroup measured fastest on C2 (finer LDS allocation granules
@@ -520,12 +516,15 @@ int32_t run_dense(const float* y, int64_t y_bstride, const float* h, int64_t h_r
                   const float* y_mean, const float* y_std, float* out, double* out_sum, double* workspace,
                   void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   DenseArgs da;
   memset(&da, 0, sizeof(da));
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
-  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMM + streaming alone
-  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // diagnostic: compute-only (first tile re-read)
+#ifdef NFN_DIAG
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // the Dense GEMM + streaming alone
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // compute-only (first tile re-read)
+#endif
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");
@@ -582,12 +581,15 @@ int32_t run_posterior_dense(const float* y, int64_t y_bstride, const float* h, i
                             int32_t trainable_base, const float* y_mean, const float* y_std, float* out,
                             double* out_sum, double* workspace, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   DenseArgs da;
   memset(&da, 0, sizeof(da));
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
-  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMMs + streaming alone
-  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // diagnostic: compute-only (first tile re-read)
+#ifdef NFN_DIAG
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // the Dense GEMMs + streaming alone
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // compute-only (first tile re-read)
+#endif
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (S < 1) return fail(NFN_E_SHAPE, "number of draws must be >= 1");
@@ -650,13 +652,16 @@ int32_t run_dense_grad(const float* y, int64_t y_bstride, const float* h, int64_
                        float* out_logp, float* grad_h, int64_t grad_h_rowstride, float* grad_W, float* grad_b,
                        float* grad_y, float* workspace, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   DenseGradArgs g;
   memset(&g, 0, sizeof(g));
   DenseArgs& da = g.da;
   ChainArgs& a = da.c;
   const int32_t P = build_program(flow_ids, K, d, trainable_base ? 1 : 0, &a.prog);
-  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // diagnostic: the Dense GEMMs + streaming alone
-  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // diagnostic: compute-only (first tile re-read)
+#ifdef NFN_DIAG
+  if (env_int("NFN_ABLATE_FLOWS", 0) == 1) a.prog.K = 0;  // the Dense GEMMs + streaming alone
+  a.ablate_loads = env_int("NFN_ABLATE_LOADS", 0) == 1 ? 1 : 0;  // compute-only (first tile re-read)
+#endif
   if (P < 0) return P;
   if (B < 0) return fail(NFN_E_SHAPE, "batch size must be >= 0");
   if (y_bstride < 0 || (y_bstride != 0 && y_bstride < d)) return fail(NFN_E_SHAPE, "bad y batch stride");
@@ -717,6 +722,7 @@ int32_t run_sample(const float* eps, int64_t eps_bstride, const float* t, int64_
                    const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                    const float* y_std, float* y_out, float* logp_out, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   SampleArgs sa;
   memset(&sa, 0, sizeof(sa));
   ChainArgs& a = sa.c;
@@ -759,6 +765,7 @@ int32_t run_grid(const float* y_grid, int64_t y_gstride, int32_t G, const float*
                  int32_t d, const int32_t* flow_ids, int32_t K, int32_t trainable_base, const float* y_mean,
                  const float* y_std, float* out, int64_t out_gstride, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   GridArgs ga;
   memset(&ga, 0, sizeof(ga));
   ChainArgs& a = ga.c;
@@ -818,21 +825,13 @@ const char* nfn_last_error(void) { return g_last_error.c_str(); }
 
 int32_t nfn_reduce_sum_f64(const double* in, int64_t n, double* out, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   if (n < 0) return fail(NFN_E_SHAPE, "n must be >= 0");
   if (!out || (n > 0 && !in)) return fail(NFN_E_NULLPTR, "in or out is NULL");
   launch_reduce_f64(in, n, out, reinterpret_cast<hipStream_t>(stream));
   return check_hip("reduce_f64_kernel launch");
 }
 
-#ifdef NFN_DIAG
-// Diagnostic build only (not in include/nfn.h): later d = 1 wave-tile launches record each
-// wave's (start, end) wall_clock64() into buf[2 w], buf[2 w + 1] (the caller sizes buf for the
-// grid); NULL stops it.  tools/wave_tail.py.
-int32_t nfn_diag_wave_times(void* buf) {
-  g_wave_times = reinterpret_cast<unsigned long long*>(buf);
-  return NFN_OK;
-}
-#endif
 
 int32_t nfn_set_launch_events(void* start_event, void* stop_event) {
   g_launch_events.start = reinterpret_cast<hipEvent_t>(start_event);
@@ -872,6 +871,7 @@ int64_t nfn_posterior_workspace_doubles(int64_t B, int32_t d, int32_t P) {
 
 int32_t nfn_reduce_partials_f64(const double* workspace, double* out_sum, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   if (!workspace || !out_sum) return fail(NFN_E_NULLPTR, "workspace or out_sum is NULL");
   launch_reduce_partials(workspace, out_sum, reinterpret_cast<hipStream_t>(stream));
   return check_hip("reduce_partials_kernel launch");
@@ -952,6 +952,7 @@ int32_t nfn_chain_logprob_grid_f32(const float* y_grid, int64_t y_gstride, int32
 int32_t nfn_flow_fwd_ldj_f32(int32_t flow_id, const float* z, int64_t z_bstride, const float* t_k,
                              int64_t t_rowstride, int64_t B, int32_t d, float* z_out, float* ldj_out, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
   const int32_t ps = param_size(flow_id, d);
   if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id));
@@ -971,6 +972,7 @@ int32_t nfn_flow_vjp_f32(int32_t flow_id, const float* z, int64_t z_bstride, con
                          int64_t B, int32_t d, const float* g_z, const float* g_ldj, float* dz_out, float* dt_out,
                          void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
   const int32_t ps = param_size(flow_id, d);
   if (ps < 0) return fail(NFN_E_FLOW_ID, "unknown flow id " + std::to_string(flow_id));
@@ -1002,6 +1004,7 @@ int32_t nfn_flow_vjp_f32(int32_t flow_id, const float* z, int64_t z_bstride, con
 int32_t nfn_split_blocks_f32(const float* t, int64_t t_rowstride, int64_t B, const int32_t* widths, int32_t nblocks,
                              float* dst, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   if (nblocks < 1 || nblocks > NFN_MAX_FLOWS) return fail(NFN_E_SHAPE, "nblocks must be in [1, " + std::to_string(NFN_MAX_FLOWS) + "]");
   if (!widths) return fail(NFN_E_NULLPTR, "widths is NULL");
   if (B < 0 || t_rowstride < 0) return fail(NFN_E_SHAPE, "negative batch or stride");
@@ -1032,6 +1035,7 @@ int32_t nfn_chain_fwd_ldj_f32(const float* z, int64_t z_bstride, const float* t,
                               int32_t d, const int32_t* flow_ids, const int32_t* block_offsets, int32_t K,
                               float* z_out, float* ldj_out, void* stream) {
   g_last_error.clear();
+  const HookScope hook_scope;
   if (d < 1 || d > NFN_MAX_DIMS) return fail(NFN_E_SHAPE, "n_dims out of range");
   if (K < 0 || K > NFN_MAX_FLOWS) return fail(NFN_E_FLOW_ID, "number of flows must be in [0, " + std::to_string(NFN_MAX_FLOWS) + "]");
   if (K > 0 && (!flow_ids || !block_offsets)) return fail(NFN_E_NULLPTR, "flow_ids or block_offsets is NULL");

@@ -67,6 +67,7 @@ int32_t nfn_comm_destroy(void* comm) {
 
 int32_t nfn_allreduce_mean(void* comm, const double* local_sum, int64_t local_count, double* sum_count,
                            double* mean_out, void* stream) {
+  const HookScope hook_scope;
   if (!comm || !local_sum || !sum_count)
     return set_error(NFN_E_NULLPTR, "nfn_allreduce_mean: NULL comm, local_sum or sum_count");
   if (local_count < 0) return set_error(NFN_E_SHAPE, "nfn_allreduce_mean: negative local_count");

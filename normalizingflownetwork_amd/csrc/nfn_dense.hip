@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   float4 buf[QH];
   float ybuf;
   auto issue = [&](int64_t tile) {
-    if (a.ablate_loads) tile = u0;  // diagnostic: compute-only timing (the first tile re-read)
+    if (diag_ablate_loads(a)) tile = u0;  // diagnostic: compute-only timing (the first tile re-read)
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     const int64_t b0c = nr > 0 ? b0 : 0;

@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
   float4 hb[4][MH];
   float ybuf, gbuf;
   auto issue = [&](int64_t tile) {
-    if (a.ablate_loads) tile = u0;  // diagnostic: compute-only timing (the first tile re-read)
+    if (diag_ablate_loads(a)) tile = u0;  // diagnostic: compute-only timing (the first tile re-read)
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     const int64_t b0c = nr > 0 ? b0 : 0;
@@ -487,6 +487,350 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-bf16 weight-gradient GEMMs (diag NFN_DGRAD_SB): chain_dense1_grad_kernel (H = 16,
+// P <= 32) with dh^T = W dt^T and dW += h^T dt on v_mfma_f32_16x16x32_bf16 instead of
+// v_mfma_f32_16x16x4_f32 (t = h W stays f32: the chain amplifies t's rounding, and a
+// split-bf16 t — a few ulp, not bitwise numpy's / the forward kernel's — put one
+// ill-conditioned sample of test_dense_grad_matches_oracle 5.4x over its dh bound,
+// profiles/r06/r06b_densetests.log).
+// Why: the f32 MFMA runs at the f32 vector rate and holds the SIMD's vector issue for all of
+// its 32 cycles, so the GEMMs serialise with the chain's VALU work
+// (profiles/r02/r02j_mfma_valu_coexec.log: 0.989 of the sum); a 16x16x32 bf16 MFMA takes 16
+// cycles and holds vector issue for 8 of them.
+// Numerics: every operand x is split EXACTLY into three bf16 parts, x = x1 + x2 + x3
+// (v_cvt_pk_bf16_f32 round-to-nearest-even, residuals exact in fp32: x1 holds 8 significant
+// bits, x2 the next 8, x3 the rest), and each product keeps the six terms x_i y_j with
+// i + j <= 4; the dropped ones (x2 y3, x3 y2, x3 y3) are below 2^-23 |x y|: fp32-level
+// products, accumulated in fp32 by the matrix cores.
+// Per 64-sample wave tile, after the chain (which is the f32 kernel's, on the f32 t tile):
+//   * each lane re-reads ITS sample's dt row; db's column sums come from the f32 tile;
+//   * h's transposed A fragments (read from the LDS h rows before the chain, as the f32
+//     kernel keeps them) are split; dW's K-slot j of lane group ak is sample
+//     32 kc + 16 (j >> 2) + 4 ak + (j & 3) (conflict-free transposed reads below);
+//   * one dt part at a time (x1, x2, x3, each split off the running residual), the part goes
+//     to a bf16 plane [sample][32] over the dead f32 tile (16-byte chunk c of row s at chunk
+//     c ^ swz(s), swz = a bit swap of (s >> 2) & 3: conflict-free row reads and transposed
+//     reads), and every product with it runs: dh^T += W_i dt_j (B = plane rows,
+//     ds_read_b128; A = W's parts, registers) and dW += h_i^T dt_j (B = the plane read
+//     transposed, ds_read_b64_tr_b16).
+// LDS per wave: the f32 kernel's (the plane needs 64 x 16 dwords).
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  const bf16x2v v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32: round to nearest even
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+// (a, b) = (hi + mi + lo) exactly, each a packed bf16 pair (element 0 = a in the low half)
+__device__ __forceinline__ void split3_pk(float a, float b, uint32_t& hi, uint32_t& mi, uint32_t& lo) {
+  hi = pk_bf16(a, b);
+  const float ra = a - bf16_lo(hi), rb = b - bf16_hi(hi);
+  mi = pk_bf16(ra, rb);
+  lo = pk_bf16(ra - bf16_lo(mi), rb - bf16_hi(mi));
+}
+__device__ __forceinline__ bf16x8v frag8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const u32x4v v = {a, b, c, d};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+__device__ __forceinline__ f32x4v mfma_bf16(bf16x8v a, bf16x8v b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// two transposed 4 x 16 reads (ds_read_b64_tr_b16 at two LDS addresses) as one fragment
+__device__ __forceinline__ bf16x8v tr_frag(const float* base0, const float* base1) {
+  const s16x4v x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4v*)((__attribute__((address_space(3))) float*)base0));
+  const s16x4v y = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4v*)((__attribute__((address_space(3))) float*)base1));
+  const s16x4v v[2] = {x, y};
+  return __builtin_bit_cast(bf16x8v, v);
+}
+// The bf16 planes' 16-byte chunk swizzle (chunk c of row r sits at chunk c ^ swz(r)): bit 0 =
+// bit 1 of the row, bit 1 = bit 2 of the row.  Checked exhaustively against the gfx950 LDS
+// lane groups (MI355X_MICROARCH.md, LDS table): conflict-free ds_read_b128 row reads (rows
+// 16 mt + am, chunk ak; the W parts' rows am), ds_read_b64_tr_b16 transposed reads (rows
+// 4 g + q of a half-wave: the two groups in different chunk pairs) and ds_write_b128 row
+// writes (one row per lane); rows r and r + 16 share the swizzle.
+__device__ __forceinline__ int dt_swz(int row) { return ((row >> 1) & 1) | ((row >> 1) & 2); }
+
+constexpr int kSbDRow = 16;   // dwords per dt-plane row (32 bf16)
+// a wave's LDS: chain_dense1_grad_kernel's (h rows / t tile + flow inputs) or the three dt planes
+__host__ __device__ inline int dense1_grad_sb_wave_floats(int P, int K) {
+  return std::max(dense1_grad_wave_floats(P, 20, K), 3 * 64 * kSbDRow);
+}
+constexpr int kSbWRow = 16;  // dwords per hidden unit of the W parts (16 pairs of p, chunks swizzled as the planes)
+constexpr int kSbWFloats = 3 * 16 * kSbWRow + 32;  // the workgroup's W bf16 parts [part][hidden][pairs of p] and bias
+
+template <int NN, int CM = kChainPairs>
+__global__ void __launch_bounds__(kMaxBlock, 3) chain_dense1_grad_sb_kernel(DenseGradArgs g) {
+  static_assert(NN == 1 || NN == 2, "P <= 32");
+  const DenseArgs& da = g.da;
+  const ChainArgs& a = da.c;
+  extern __shared__ float lds[];
+  constexpr int H = 16;
+  constexpr int QH = 4;
+  constexpr int SH = H + 4;  // h rows in LDS (as chain_dense1_grad_kernel)
+  constexpr int NP = 16 * NN;
+  constexpr int kNT = 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwave = blockDim.x >> 6;
+  const int P = a.P;
+  const int K = a.prog.K;
+  const int wfl = dense1_grad_sb_wave_floats(P, K);  // the f32 kernel's region, or the three dt planes
+  float* const wb = lds + wid * wfl;
+  float* const tl = wb;  // t / dt tile, column-major; the h rows overlay it, then the dt plane
+  float* const hl = wb;
+  float* const zh = tl + (P + 2) * kCS + lane;
+  const int am = lane & 15, ak = lane >> 4;
+
+  // t = h W (f32 MFMA, bitwise chain_dense1_kernel's t): B fragments W[hidden 4 ks + ak][p]
+  // (registers); the bias from the workgroup's LDS copy (after the W parts), read per tile
+  float wB[QH][NN];
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    const int p = 16 * nt + am;
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks) wB[ks][nt] = p < P ? da.W[(4 * ks + ak) * P + p] : 0.0f;
+  }
+  float* const bl = lds + nwave * wfl + 3 * 16 * kSbWRow;
+  for (int i = tid; i < NP; i += blockDim.x) bl[i] = (i < P && da.bias) ? da.bias[i] : 0.0f;
+  // dh^T = W dt^T (bf16 parts): A fragments W_i[hidden am][p = 8 ak + j], i = 1, 2, 3, in the
+  // workgroup's LDS after the waves' regions ([part][hidden][kSbWRow]), read per use
+  uint32_t* const wpl = reinterpret_cast<uint32_t*>(lds + nwave * wfl);
+  for (int i = tid; i < 16 * 16; i += blockDim.x) {
+    const int hh = i >> 4, q = i & 15, p = 2 * q;
+    const float x0 = p < P ? da.W[hh * P + p] : 0.0f, x1 = p + 1 < P ? da.W[hh * P + p + 1] : 0.0f;
+    uint32_t w1, w2, w3;
+    split3_pk(x0, x1, w1, w2, w3);
+    const int at = hh * kSbWRow + 4 * ((q >> 2) ^ dt_swz(hh)) + (q & 3);
+    wpl[at] = w1;
+    wpl[16 * kSbWRow + at] = w2;
+    wpl[32 * kSbWRow + at] = w3;
+  }
+  __syncthreads();
+  const int64_t hs = da.h_rowstride;
+  const int64_t ghs = g.gh_rowstride;
+  const int64_t ntiles = a.ntiles;
+  const int64_t u0 = (int64_t)blockIdx.x * nwave + wid;
+  const int64_t ustep = (int64_t)gridDim.x * nwave;
+  const bool norm = a.y_mean != nullptr;
+  float ymean = 0.0f, ystd = 1.0f, corr = 0.0f;
+  if (norm) {
+    ymean = a.y_mean[0];
+    ystd = a.y_std[0];
+    corr = f_log<true>(ystd);
+  }
+  const bool trainable = a.trainable != 0;
+  const uint32_t types = a.prog.types[0];
+  const int yoff = lane * (int)a.y_bstride * 4;
+  const int hoff = (am * (int)hs + 4 * ak) * 4;
+  const int hmt = 16 * (int)hs * 4;
+  const int ghoff = (am * (int)ghs + 4 * ak) * 4;
+  const int ghmt = 16 * (int)ghs * 4;
+  // transposed reads: lane 4 q + p' of group ak supplies row q, columns 4 p' .. 4 p' + 3
+  const int trq = (lane & 15) >> 2, trp = lane & 3;
+  const int swz_w = dt_swz(am);  // plane-row reads: rows 16 mt + am share their low 4 bits with am
+  const int swz_l = dt_swz(lane);
+
+  float4 hb[4];
+  float ybuf, gbuf;
+  auto issue = [&](int64_t tile) {
+    if (diag_ablate_loads(a)) tile = u0;  // diagnostic: compute-only timing (the first tile re-read)
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    const int64_t b0c = nr > 0 ? b0 : 0;
+    const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
+    const auto rg = tile_rsrc(g.g_out ? g.g_out + b0c : a.y, g.g_out ? nr * 4 : 0);
+    gbuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lane * 4, 0, 0));
+    const auto rh = tile_rsrc(da.h + b0c * hs, nr > 0 ? ((nr - 1) * hs + H) * 4 : 0);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+      hb[mt] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, mt * hmt, kNT));
+  };
+
+  f32x4v dw[NN];
+  float db[NN];
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    db[nt] = 0.0f;
+    dw[nt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+
+  issue(u0);
+  for (int64_t tile = u0; tile < ntiles; tile += ustep) {
+    const int64_t b0 = tile * 64;
+    const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    // 1. h rows -> LDS (row-major); read back: t = h W's A fragments and, transposed, dW's
+    //    h[sample 32 kc + 16 (j >> 2) + 4 ak + (j & 3)][hidden am] (kept in registers)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) *reinterpret_cast<float4*>(hl + (16 * mt + am) * SH + 4 * ak) = hb[mt];
+    const float z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
+    const float gl = g.g_out ? gbuf : 1.0f;
+    wave_lds_sync();
+    issue(tile + ustep);  // the next tile's loads (hb is free once in LDS)
+    float av[4][QH], hA[16];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < QH; ++ks) av[mt][ks] = hl[(16 * mt + am) * SH + 4 * ks + ak];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) hA[j] = hl[(32 * (j >> 3) + 16 * ((j >> 2) & 1) + 4 * ak + (j & 3)) * SH + am];
+    wave_lds_sync();  // every h read done before the t tile overwrites the rows
+    // 2. t = h W + b (f32 MFMA)
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) {
+      f32x4v acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < QH; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt][ks], wB[ks][nt], acc[mt], 0, 0, 0);
+      if (16 * nt + am < P) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          *reinterpret_cast<f32x4v*>(tl + (16 * nt + am) * kCS + 16 * mt + 4 * ak) = acc[mt] + bl[16 * nt + am];
+      }
+    }
+    wave_lds_sync();
+    // 3. the chain forward + reverse per lane: the t column entries become g * d logp / d t
+    float adj, z = z0;
+    float lp;
+    if constexpr (CM >= kChainHPair)
+      lp = grad1_hpairs<((CM - kChainHPair) % 9) / 3, (CM - kChainHPair) % 3, kCS>(
+               z, tl + lane, zh, 64, K, P, trainable, gl, a.out != nullptr, adj) - corr;
+    else if constexpr (CM == kChainPairs)
+      lp = grad1_pairs<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
+    else
+      lp = grad1_packed<kCS>(z, tl + lane, zh, 64, types, K, P, trainable, gl, a.out != nullptr, adj) - corr;
+    {
+      const auto ro = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, lp), ro, lane * 4, 0, kNT);
+      const auto rdy = tile_rsrc(g.grad_y && nr > 0 ? g.grad_y + b0 : g.grad_y, g.grad_y ? nr * 4 : 0);
+      const float gy = norm ? f_div<true>(adj, ystd) : adj;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, gy), rdy, lane * 4, 0, kNT);
+    }
+    // 4. this lane's dt row and db's column sums, from the f32 tile (rows past B carry no
+    //    gradient: zeroed first, as in chain_dense1_grad_kernel)
+    if (nr < 64 && lane >= nr) {
+      for (int p = 0; p < P; ++p) tl[p * kCS + lane] = 0.0f;
+    }
+    float v[32];  // the dt row
+#pragma unroll
+    for (int p = 0; p < 32; ++p) v[p] = (p < NP && p < P) ? tl[p * kCS + lane] : 0.0f;
+    wave_lds_sync();  // the chain's dt writes (other lanes' columns) are visible to the column reads
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) {
+      const bool col = 16 * nt + am < P;
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) {
+        f32x4v q = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+        if (col) q = *reinterpret_cast<const f32x4v*>(tl + (16 * nt + am) * kCS + 16 * kq + 4 * ak);
+        db[nt] += (q[0] + q[1]) + (q[2] + q[3]);
+      }
+    }
+    // 5. dt's three bf16 parts -> three planes [sample][32] over the dead f32 tile (16-byte
+    //    chunk c of row s at chunk c ^ swz(s))
+    wave_lds_sync();  // every f32 read done before the planes overwrite the tile
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t d1[4], d2[4], d3[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split3_pk(v[8 * c + 2 * q], v[8 * c + 2 * q + 1], d1[q], d2[q], d3[q]);
+      float* row = wb + lane * kSbDRow + 4 * (c ^ swz_l);
+      *reinterpret_cast<u32x4v*>(row) = u32x4v{d1[0], d1[1], d1[2], d1[3]};
+      *reinterpret_cast<u32x4v*>(row + 64 * kSbDRow) = u32x4v{d2[0], d2[1], d2[2], d2[3]};
+      *reinterpret_cast<u32x4v*>(row + 128 * kSbDRow) = u32x4v{d3[0], d3[1], d3[2], d3[3]};
+    }
+    wave_lds_sync();
+    // 6. dh^T = W dt^T (B = plane rows): lane (am, ak) ends with dh[16 mt + am][4 ak .. 4 ak + 3];
+    //    the six terms small first: (3,1) (2,2) (1,3) (2,1) (1,2) (1,1)
+    {
+      const auto rdh = tile_rsrc(g.grad_h && nr > 0 ? g.grad_h + b0 * ghs : g.grad_h,
+                                 g.grad_h && nr > 0 ? ((nr - 1) * ghs + H) * 4 : 0);
+      const uint32_t* wr = wpl + am * kSbWRow + 4 * (ak ^ swz_w);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const float* row = wb + (16 * mt + am) * kSbDRow + 4 * (ak ^ swz_w);
+        const bf16x8v d1 = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(row));
+        const bf16x8v d2 = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(row + 64 * kSbDRow));
+        const bf16x8v d3 = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(row + 128 * kSbDRow));
+        const bf16x8v w1 = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(wr));
+        const bf16x8v w2 = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(wr + 16 * kSbWRow));
+        const bf16x8v w3 = __builtin_bit_cast(bf16x8v, *reinterpret_cast<const u32x4v*>(wr + 32 * kSbWRow));
+        f32x4v acc = mfma_bf16(w3, d1, f32x4v{0.0f, 0.0f, 0.0f, 0.0f});
+        acc = mfma_bf16(w2, d2, acc);
+        acc = mfma_bf16(w1, d3, acc);
+        acc = mfma_bf16(w2, d1, acc);
+        acc = mfma_bf16(w1, d2, acc);
+        acc = mfma_bf16(w1, d1, acc);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, acc), rdh, ghoff, mt * ghmt, kNT);
+      }
+    }
+    // 7. dW += h^T dt: A = h's parts (split from the transposed reads kept since step 1),
+    //    B = the planes read transposed [8 samples][16 columns]
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      uint32_t x1[4], x2[4], x3[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) split3_pk(hA[8 * kc + 2 * q], hA[8 * kc + 2 * q + 1], x1[q], x2[q], x3[q]);
+      const bf16x8v h1 = frag8(x1[0], x1[1], x1[2], x1[3]);
+      const bf16x8v h2 = frag8(x2[0], x2[1], x2[2], x2[3]);
+      const bf16x8v h3 = frag8(x3[0], x3[1], x3[2], x3[3]);
+      const int r = 32 * kc + 4 * ak + trq;  // r and r + 16 share the swizzle
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt) {
+        const float* bp = wb + r * kSbDRow + 4 * ((2 * nt + (trp >> 1)) ^ dt_swz(r)) + 2 * (trp & 1);
+        const bf16x8v e1 = tr_frag(bp, bp + 16 * kSbDRow);
+        const bf16x8v e2 = tr_frag(bp + 64 * kSbDRow, bp + 80 * kSbDRow);
+        const bf16x8v e3 = tr_frag(bp + 128 * kSbDRow, bp + 144 * kSbDRow);
+        f32x4v acc = dw[nt];
+        acc = mfma_bf16(h3, e1, acc);
+        acc = mfma_bf16(h2, e2, acc);
+        acc = mfma_bf16(h1, e3, acc);
+        acc = mfma_bf16(h2, e1, acc);
+        acc = mfma_bf16(h1, e2, acc);
+        dw[nt] = mfma_bf16(h1, e1, acc);
+      }
+    }
+    wave_lds_sync();  // this tile's LDS reads done before the next tile's writes
+  }
+  if (g.part == nullptr) return;  // no grad_W / grad_b requested (uniform: every thread returns)
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    db[nt] += __shfl_xor(db[nt], 16);
+    db[nt] += __shfl_xor(db[nt], 32);
+  }
+  const int nWb = H * P + P;
+  __syncthreads();
+  float* mine = lds + wid * wfl;
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hr = 4 * ak + i, p = 16 * nt + am;  // C layout: row 4 ak + i, column am
+      if (p < P) mine[hr * P + p] = dw[nt][i];
+    }
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt)
+    if (ak == 0 && 16 * nt + am < P) mine[H * P + 16 * nt + am] = db[nt];
+  __syncthreads();
+  float* out = g.part + (int64_t)blockIdx.x * nWb;
+  for (int i = tid; i < nWb; i += blockDim.x) {
+    float s = lds[i];
+    for (int w = 1; w < nwave; ++w) s += lds[w * wfl + i];
+    out[i] = s;
+  }
+}
+
 // grad_W | grad_b = the sum of the per-workgroup partials (fp64, deterministic): a
 // workgroup owns 64 consecutive elements (lane = element, coalesced rows of the
 // partials); its 16 waves take the partials w, w + 16, ... and are combined in wave order
@@ -539,8 +883,26 @@ int64_t launch_dg1(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
   return grid;
 }
 
+// the split-bf16 form (H = 16, P <= 32); kDgradSplitBf16 = its release default, diag NFN_DGRAD_SB
+constexpr int kDgradSplitBf16 = 1;
+template <int NN>
+int64_t launch_dg1_sb(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
+  auto kfn = chain_dense1_grad_sb_kernel<NN, kChainPairs>;
+#ifdef NFN_DIAG
+  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop) kfn = chain_dense1_grad_sb_kernel<NN, kChainLoop>;
+#endif
+  const size_t lds = ((size_t)4 * dense1_grad_sb_wave_floats(g.da.c.P, g.da.c.prog.K) + kSbWFloats) * sizeof(float);
+  int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);
+  grid = std::max<int64_t>(1, std::min<int64_t>(grid, max_parts));
+  nfn_launch(kfn, dim3((unsigned)grid), dim3(kMaxBlock), lds, s, g);
+  return grid;
+}
+
 template <int MH>
 int64_t launch_dg1_n(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
+  if (MH == 1 && g.da.c.P <= 32 && env_int("NFN_DGRAD_SB", kDgradSplitBf16) != 0 &&
+      ((size_t)4 * dense1_grad_sb_wave_floats(g.da.c.P, g.da.c.prog.K) + kSbWFloats) * sizeof(float) <= (size_t)64 * 1024)
+    return g.da.c.P <= 16 ? launch_dg1_sb<1>(g, max_parts, s) : launch_dg1_sb<2>(g, max_parts, s);
   switch ((g.da.c.P + 15) / 16) {
     case 1: return launch_dg1<MH, 1>(g, max_parts, s);
     case 2: return launch_dg1<MH, 2>(g, max_parts, s);

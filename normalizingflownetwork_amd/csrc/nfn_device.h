@@ -105,22 +105,18 @@ struct ChainArgs {
   int64_t ntiles;      // persistent kernel: number of `blockDim.x`-row tiles
   int32_t nt;          // non-temporal parameter-row loads
   int32_t nt_store;    // non-temporal log_prob stores
-  int32_t ablate_loads;  // diagnostic: stream only the first tile (compute-only timing)
   int32_t nsplit;      // posterior: draw ranges per tile (1 = no split)
   int32_t dps;         // posterior: draws per range
   float2* split_out;   // posterior split: (max, scaled sum) per (range, sample)
   int32_t tile_rows;   // tile kernels: samples per tile when < blockDim.x (very wide rows)
-  int32_t prio;        // tuning: raise wave priority around the tile hand-off (NFN_PRIO)
-  int32_t load_aux;    // diagnostic (NFN_LOAD_AUX, diag builds): chain_wave1_kernel's row-load cache policy
-  int32_t store_aux;   // diagnostic (NFN_STORE_AUX, diag builds): the forward kernels' log_prob store cache policy (store_out32)
-  int32_t pace_rand;   // diagnostic (NFN_PACE_RAND, diag builds): a pseudo-random s_sleep count per wave tile
-  int32_t pace;        // diagnostic (NFN_PACE, diag builds): per wave tile in chain_wave1_kernel, s_sleep(1) x pace (> 0) or -16 pace fma in 8 independent chains (< 0)
-  int32_t split_issue; // diagnostic (NFN_SPLIT_ISSUE, diag builds): launch selects chain_wave1_kernel<..., SPLIT = true>
-  unsigned long long* wave_times;  // diagnostic (nfn_diag_wave_times, diag builds): chain_wave1_kernel's per-wave (start, end) wall clock
-  int32_t tile_rot;    // chain_wave1_kernel: step k's tile slot for wave w is (w + k tile_rot) mod waves (0 = w)
-  int32_t tile_rot_g;  // the same for chain_group1_kernel
-  int32_t xcd_skew;    // chain_wave1_kernel: the last xcd_skew steps split 3 : 1 between even- and odd-XCD waves (0 = evenly)
-  int32_t early_issue; // diagnostic (NFN_EARLY_ISSUE, diag builds): chain_wave1_kernel issues the next tile before the hand-off's LDS wait
+  int32_t prio;        // raise wave priority around the tile hand-off (1 in the release library)
+  int32_t tile_rot;    // chain_wave1_kernel: step k's tile slot for wave w is (w + k tile_rot) mod waves (>= 0)
+#ifdef NFN_DIAG
+  // diagnostic build only (libnfn_hip_diag.so; the release kernels compile these paths out)
+  int32_t ablate_loads;  // NFN_ABLATE_LOADS: stream only the first tile (compute-only timing)
+  int32_t tile_rot_g;    // NFN_TILE_ROT_G: chain_group1_kernel's rotated slots (release: the plain walk)
+  int32_t tile_rot_b;    // NFN_TILE_ROT_B: chain_grad_wave_kernel's rotated slots (release: the plain walk)
+#endif
   int64_t grid_cap;    // > 0: persistent grids are capped here (the workspace's partial slots)
   float* z_out;        // Chain bijector form (chain_wave1_kernel<..., FWD>): z_K per sample
   int32_t zonly;       // backward: z-only forward recompute when no log_prob is wanted (tuning knob)
@@ -128,6 +124,18 @@ struct ChainArgs {
   uint32_t epoch;      // summed launch: this call's ticket epoch (non-zero, see write_partial)
   FlowProgram prog;
 };
+
+// The diagnostic build's knobs (ChainArgs' NFN_DIAG block); the release library sees the
+// constants, so every such path folds away at compile time.
+#ifdef NFN_DIAG
+__host__ __device__ inline bool diag_ablate_loads(const ChainArgs& a) { return a.ablate_loads != 0; }
+__host__ __device__ inline int diag_tile_rot_g(const ChainArgs& a) { return a.tile_rot_g; }
+__host__ __device__ inline int diag_tile_rot_b(const ChainArgs& a) { return a.tile_rot_b; }
+#else
+__host__ __device__ inline bool diag_ablate_loads(const ChainArgs&) { return false; }
+__host__ __device__ inline int diag_tile_rot_g(const ChainArgs&) { return 0; }
+__host__ __device__ inline int diag_tile_rot_b(const ChainArgs&) { return 0; }
+#endif
 
 // Output Dense layer fused into the chain (nfn_dense.hip): t = h W + b on chip.
 struct DenseArgs {
@@ -278,7 +286,8 @@ __device__ __forceinline__ float softplus_alpha(float x) {
 // Below |a| = 0.3 an odd polynomial (tanh(a) / a - 1 as three terms in a^2, fitted for relative
 // error on [0, 0.3]: <= 0.69 ulp, 0.26 on average); above it 1 - 2 / (1 + e^{2|a|}) with the
 // sign copied back (<= 2.9 ulp on [0.3, 1), <= 1.2 past 1; e^{2|a|} -> inf saturates to 1; ulp
-// figures with correctly rounded v_exp / v_rcp, both signs alike).  Evaluating the exp form
+// figures with correctly rounded v_exp / v_rcp, both signs alike; with the hardware's, measured
+// on MI355X: 3.19 ulp at most on [-1, 1], pinned at 3.25 by tests/test_gpu_diag.py).  Evaluating the exp form
 // at |a| is what round 4's accuracy gain came from: round 3 evaluated it at signed a, where
 // 2 / (1 + e^{2a}) > 1 has twice the ulp (5.2 ulp).  Round 4's five-term polynomial on [0, 0.55]
 // bought nothing over this one in the fp32 emulation of the C2 chain (tools/kernel_emu.py: 200
@@ -730,22 +739,6 @@ __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, 
   return l2;
 }
 
-// n pairs of an alternating program from the block ending at `off` (advanced): the U = 1 body
-// of chain1_fast_hpairs, so two calls over [0, h) and [h, K / 2) plus the odd tail give its
-// values bitwise (chain_wave1_kernel<..., SPLIT>: the next tile's second half issues between).
-template <int IA, int IB, int ST = 1>
-__device__ __forceinline__ void hpairs_range(float& z, float& l2, const float* row, int& off, int n) {
-  constexpr int SA = IA == NFN_FLOW_AFFINE ? 2 : 3, SB = IB == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + SB;
-#pragma unroll 1
-  for (int p = 0; p < n; ++p) {
-    float pa[3], pb[3];
-    read3c<ST>(pa, row, off - SA);
-    read3c<ST>(pb, row, off - SP);
-    flow_pair1<IA, IB>(z, l2, pa, pb);
-    off -= SP;
-  }
-}
-
 // chain1_fast_pairs over TWO rows that share the program (two draws of one sample in the
 // posterior): one dispatch per pair of flows for both, two independent dependency chains
 // for the scheduler to interleave.  Per row the same arithmetic as chain1_fast_pairs.
@@ -1183,7 +1176,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_persistent_kernel(ChainArg
     const int64_t b0 = tile * TR;
     const int nr = (int)min((int64_t)TR, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
-    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    if (diag_ablate_loads(a) && issued_once) return;  // diagnostic: compute-only timing
     issued_once = true;
     if (a.nt) {
 #pragma unroll
@@ -1341,38 +1334,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
 // compile-time pair bodies runs 0.378-0.380 ms with sc1 stores against 0.389-0.391 with nt
 // (three boxes, profiles/r05/r05u / r05v / r05w_*), C3 -0.5 %, C5 unchanged; the memory-only
 // form gains the same 2.5 %.  (The backward's gradient stores stay nt: a backward-shaped stream
-// gains nothing from sc1, r05w_mixed_stream.log.)  The diagnostic build takes NFN_STORE_AUX
-// (a.store_aux: 0, 2, 16 or 18; -1 = kOutAux) for A/B studies.
+// gains nothing from sc1, r05w_mixed_stream.log.)
 constexpr int kOutAux = 16;
-__device__ __forceinline__ void store_out32(float v, __amdgpu_buffer_rsrc_t r, int off, const ChainArgs& a) {
-  const uint32_t u = __builtin_bit_cast(uint32_t, v);
-#ifdef NFN_DIAG
-  switch (a.store_aux) {
-    case 0: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 0); return;
-    case 2: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 2); return;
-    case 16: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 16); return;
-    case 18: __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, 18); return;
-    default: break;
-  }
-#else
-  (void)a;
-#endif
-  __builtin_amdgcn_raw_buffer_store_b32(u, r, off, 0, kOutAux);
+__device__ __forceinline__ void store_out32(float v, __amdgpu_buffer_rsrc_t r, int off, const ChainArgs&) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kOutAux);
 }
 
 // FWD: the Bijector API's Chain forward + forward_log_det_jacobian instead of log_prob
 // (nfn_chain_fwd_ldj_f32 over the layer's flow blocks; needs FAST and PACKED): z_K goes to
 // a.z_out and sum_k log|det J_k| to a.out; no base density, no partial sums.
-// DMA (diagnostic A/B, NFN_DIAG builds: NFN_WAVE1_DMA=1): the tile's rows go global -> LDS
-// by LDS-DMA (buffer_load_dword ... lds, non-temporal), one instruction per row (the
-// row's P dwords, lanes 0..P-1) so the odd row stride and every read stay as they are,
-// into the other of two LDS slots per wave while the chain reads the current one; no
-// register prefetch, no ds_write hand-off.  The next hand-off waits with an explicit
-// vmcnt(1) (hipcc does not order a ds_read behind an LDS-DMA).
-template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop, bool DMA = false, bool SPLIT = false>
+// (Round 5's rejected studies of this loop — LDS-DMA row fill, split / early issue, load and
+// store cache policies, pacing, XCD skew, per-wave timestamps — are documented in DESIGN.md
+// with their logs under profiles/r05/; they are no longer compiled.)
+template <bool FAST, int Q, bool PACKED, bool FWD = false, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) {
-  static_assert(!SPLIT || (FAST && !FWD && !DMA && CM >= kChainHPair && (CM - kChainHPair) / 9 == 1),
-                "SPLIT: the diagnostic split issue runs the U = 1 pair bodies of the log_prob form");
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
   constexpr int RSTEP = 64 / Q;  // rows per wave-instruction
@@ -1382,8 +1357,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   const int S = a.lds_stride;
   const int64_t rs = a.t_rowstride;
   const int r0 = lane / Q, c4 = lane % Q;
-  float* tl = lds + wid * 64 * S * (DMA ? 2 : 1);
-  float* tl_next = tl + 64 * S;  // DMA: the slot the next tile lands in
+  float* tl = lds + wid * 64 * S;
   const int l0 = r0 * S + 4 * c4;
   const int64_t ntiles = a.ntiles;
   const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -1395,11 +1369,8 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     ystd = a.y_std[0];
     corr = f_log<FAST>(ystd);
   }
-  // diagnostic (NFN_ABLATE_LOADS): every tile re-reads the wave's first tile
-  const int64_t abl_tile = a.ablate_loads ? u0 : -1;
-#ifdef NFN_DIAG
-  const unsigned long long wt0 = a.wave_times ? wall_clock64() : 0ull;  // tail study (nfn_diag_wave_times)
-#endif
+  // diagnostic build (NFN_ABLATE_LOADS): every tile re-reads the wave's first tile
+  const int64_t abl_tile = diag_ablate_loads(a) ? u0 : -1;
   // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
   const int yoff = lane * (int)a.y_bstride * 4;
   const int toff = (r0 * (int)rs + 4 * c4) * 4;
@@ -1408,60 +1379,19 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   // Tiles past the end are issued too, through empty descriptors (no memory traffic,
   // zeros returned): every path then holds the same loads in the same order and the
   // waitcnt pass counts each hand-off's wait exactly.
-  float4 buf[DMA ? 1 : Q];
+  float4 buf[Q];
   float ybuf;
-  // part: 2 = the whole tile; SPLIT's halves 0 = y + the first Q / 2 row pieces, 1 = the rest
-  auto issue = [&](int64_t tile, int part = 2) {
+  auto issue = [&](int64_t tile) {
     if (abl_tile >= 0) tile = abl_tile;
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     const int64_t b0c = nr > 0 ? b0 : 0;
     const auto ry = tile_rsrc(a.y + b0c * a.y_bstride, nr > 0 ? ((nr - 1) * a.y_bstride + 1) * 4 : 0);
     const auto rt = tile_rsrc(a.t + b0c * rs, nr > 0 ? ((nr - 1) * rs + a.P) * 4 : 0);
-    if constexpr (DMA) {
-      // rows first, y last: the hand-off's wait for y (and its vmcnt(1)) covers them
-      if (lane < 4 * Q) {
+    ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
 #pragma unroll
-        for (int r = 0; r < 64; ++r)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(tl_next + r * S), 4,
-                                                   lane * 4, r * (int)rs * 4, 0, kNT);
-      }
-      ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
-    } else {
-#ifdef NFN_DIAG
-      // load-policy study, one branch that returns (the default path below stays straight-line):
-      // NFN_LOAD_AUX 102 / 116 = y nt / sc1 (rows nt); 16 / 18 / 3 = rows sc1 / sc1 nt / sc0 nt
-      if constexpr (!SPLIT) {
-        const int la = a.load_aux;
-        if (la == 102 || la == 116 || la == 16 || la == 18 || la == 3) {
-          const int ya = la == 102 ? 2 : la == 116 ? 16 : 0, ta = la >= 100 ? kNT : la;
-          if (ya == 2)
-            ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 2));
-          else if (ya == 16)
-            ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 16));
-          else
-            ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
-#pragma unroll
-          for (int k = 0; k < Q; ++k) {
-            if (ta == 16)
-              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 16));
-            else if (ta == 18)
-              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 18));
-            else if (ta == 3)
-              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, 3));
-            else
-              buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
-          }
-          return;
-        }
-      }
-#endif
-      if (part != 1) ybuf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, yoff, 0, 0));
-#pragma unroll
-      for (int k = 0; k < Q; ++k)
-        if (part == 2 || (k < Q / 2) == (part == 0))
-          buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
-    }
+    for (int k = 0; k < Q; ++k)
+      buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, toff, k * kstep, kNT));
   };
 
   double acc = 0.0;
@@ -1479,97 +1409,33 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
   // Step k covers tiles [k W, (k + 1) W) (W = ustep, the grid's waves); the wave takes slot
   // (u0 + k rot) mod W of it, so with rot > 0 a workgroup's waves visit every part of each
   // step's address range in turn instead of always the same one.
-  // (The slot advances incrementally: rot < W, no division.)
+  // (The slot advances incrementally: 0 <= rot < W, no division.)
   const int64_t rot = a.tile_rot % ustep;
-  // XCD skew (a.xcd_skew = L > 0, even): the last L steps' L W tiles are not split evenly but
-  // 3 : 1 between the waves of even- and odd-numbered XCDs (workgroup b runs on XCD b mod 8),
-  // which finish their equal shares ~4 % apart (tools/wave_tail.py): an even-XCD wave takes 3L/2
-  // tiles of that block, an odd-XCD wave L/2.  Whole steps only (ntiles a multiple of W).
-  int64_t kf = INT64_MAX, soff = 0, scnt = 0;
-  const int64_t half = ustep >> 1;
-  if (a.xcd_skew > 0 && (a.xcd_skew & 1) == 0 && (gridDim.x & 7) == 0 && ntiles % ustep == 0 &&
-      ntiles / ustep > a.xcd_skew) {
-    const int L = a.xcd_skew;
-    const int b = blockIdx.x, x = b & 7, nwb = blockDim.x >> 6;
-    const int64_t rank = ((int64_t)(b >> 3) * 4 + (x >> 1)) * nwb + wid;  // among the even (odd) XCDs' waves
-    kf = ntiles / ustep - L;
-    scnt = (x & 1) ? L / 2 : 3 * L / 2;
-    soff = kf * ustep + ((x & 1) ? 3 * (int64_t)L * half / 2 : 0) + rank;
-  }
   issue(u0);
   flush();  // empty: every path into the loop ends [loads][store] (counted waits)
-  for (int64_t tile = u0, base = 0, slot = u0, step = 0, tnext; tile < ntiles; tile = tnext, ++step) {
-    if (step + 1 < kf) {
-      slot += rot;
-      if (slot >= ustep) slot -= ustep;
-      base += ustep;
-      tnext = base + slot;  // the next step's tile
-    } else {
-      const int64_t m = step + 1 - kf;  // the next tile's place in this wave's share of the skewed block
-      tnext = m < scnt ? soff + m * half : ntiles;
-    }
+  for (int64_t tile = u0, base = 0, slot = u0, tnext; tile < ntiles; tile = tnext) {
+    slot += rot;
+    if (slot >= ustep) slot -= ustep;
+    base += ustep;
+    tnext = base + slot;  // the next step's tile
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     if (a.prio) __builtin_amdgcn_s_setprio(3);  // hand-off + next prefetch at high priority
-    if constexpr (DMA) {
-      // this tile's rows (issued before its y) have landed; only the last store may be
-      // outstanding.  Then the slots swap: the chain reads what just landed, the next
-      // tile's rows go to the slot the previous chain finished reading (wave_lds_sync)
-      if constexpr (FWD)
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // flush() issues two stores
-      else
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      float* const t_ = tl;
-      tl = tl_next;
-      tl_next = t_;
-    } else {
 #pragma unroll
-      for (int k = 0; k < Q; ++k) {
-        float* dst = tl + l0 + k * RSTEP * S;
-        dst[0] = buf[k].x;
-        dst[1] = buf[k].y;
-        dst[2] = buf[k].z;
-        dst[3] = buf[k].w;
-      }
+    for (int k = 0; k < Q; ++k) {
+      float* dst = tl + l0 + k * RSTEP * S;
+      dst[0] = buf[k].x;
+      dst[1] = buf[k].y;
+      dst[2] = buf[k].z;
+      dst[3] = buf[k].w;
     }
     const float z0 = norm ? f_div<FAST>(ybuf - ymean, ystd) : ybuf;
-#ifdef NFN_DIAG
-    if (SPLIT) {
-      wave_lds_sync();
-      issue(tnext, 0);
-    } else if (a.early_issue) {  // the next tile's loads go out behind the ds_writes, before their wait
-      issue(tnext);
-      flush();
-      wave_lds_sync();
-    } else
-#endif
-    {
-      wave_lds_sync();
-      issue(tnext);
-      flush();
-    }
+    wave_lds_sync();
+    issue(tnext);
+    flush();
     if (a.prio) __builtin_amdgcn_s_setprio(0);
     float lp;
-    if constexpr (SPLIT) {
-      // diagnostic: the next tile's second half issues after the first half of the pairs, so
-      // a wave holds ~half a tile in flight once the first half has landed
-      constexpr int c = CM - kChainHPair;
-      constexpr int IA = (c % 9) / 3, IB = c % 3;
-      const float* row = tl + lane * S;
-      float z = z0, l2 = 0.0f;
-      int off = a.P;
-      const int np = a.prog.K >> 1, h = np >> 1;
-      hpairs_range<IA, IB>(z, l2, row, off, h);
-      issue(tnext, 1);
-      flush();
-      hpairs_range<IA, IB>(z, l2, row, off, np - h);
-      if (a.prog.K & 1) {
-        float pa[3];
-        read3c(pa, row, off - (IA == NFN_FLOW_AFFINE ? 2 : 3));
-        l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
-      }
-      lp = base1_fast(z, row, a.trainable != 0) + l2 * kLn2 - corr;
-    } else if constexpr (FWD) {
+    if constexpr (FWD) {
       static_assert(FAST && PACKED, "the Chain bijector form uses the packed fast-math chain");
       float z = z0;
       lp = (a.prog.K > 0 ? chain1_fast_packed(z, tl + lane * S, a.prog.types[0], a.prog.K, a.P) : 0.0f) * kLn2;
@@ -1587,37 +1453,9 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_wave1_kernel(ChainArgs a) 
     }
     pend_v = lp;
     pend_r = tile_rsrc(a.out && nr > 0 ? a.out + b0 : a.out, a.out ? nr * 4 : 0);
-#ifdef NFN_DIAG
-    // pacing study: pace > 0 sleeps (s_sleep 1, ~64 cycles each), pace < 0 issues -pace x 16
-    // v_fma_f32 in eight independent chains whose results are kept (busy VALU, no memory)
-    for (int i = 0; i < a.pace; ++i) __builtin_amdgcn_s_sleep(1);
-    if (a.pace_rand > 0) {  // a pseudo-random number of s_sleep(1) in [0, pace_rand) per (wave, tile)
-      const uint32_t h = (uint32_t)tile * 2654435761u ^ (uint32_t)(blockIdx.x * 8 + wid) * 40503u;
-      const int n = (int)((h >> 13) % (uint32_t)a.pace_rand);
-      for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
-    }
-    if (a.pace < 0) {  // -pace x 16 fma in 8 independent chains (the VALU busy, not waiting)
-      float x[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = lp + (float)j;
-      for (int i = 0; i < -2 * a.pace; ++i) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = fmaf(x[j], 0.999f, 0.5f);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(x[j]));
-    }
-#endif
     wave_lds_sync();  // this tile's LDS reads done before the next writes
   }
   flush();
-#ifdef NFN_DIAG
-  if (a.wave_times && lane == 0) {  // vector stores of this wave's (start, end)
-    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wid;
-    a.wave_times[2 * gw] = wt0;
-    a.wave_times[2 * gw + 1] = wall_clock64();
-  }
-#endif
   if (a.partials) {
     write_partial(a.partials, acc, nfc, red, a.out_sum, a.epoch, a.pair_base);
   }
@@ -2137,7 +1975,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group_kernel(ChainArgs a) {
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
     const float* base = a.t + (int64_t)s * a.t_drawstride + b0 * rs;
-    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    if (diag_ablate_loads(a) && issued_once) return;  // diagnostic: compute-only timing
     issued_once = true;
     int r = r00, c = c00;
 #pragma unroll
@@ -2276,7 +2114,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   const int64_t ustep = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int tbytes = R * a.P * 4;  // one full tile (< 2 GiB: P <= 2^24 / R)
   const int64_t ybs = a.y_bstride;
-  const int abl = a.ablate_loads;
+  const bool abl = diag_ablate_loads(a);
   float4 buf[NV];
   float ybuf[DPL];
   auto issue = [&](int64_t tile) {
@@ -2311,8 +2149,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_group1_kernel(ChainArgs a) {
   int nfc = 0;  // non-finite log_prob values
   __amdgpu_buffer_rsrc_t pend_r = tile_rsrc(a.out, 0);
   float pend_v = 0.0f;
-  // rotated tile slots as in chain_wave1_kernel (a.tile_rot_g)
-  const int64_t rot = a.tile_rot_g % ustep;
+  // rotated tile slots as in chain_wave1_kernel: the plain walk (rot = 0) in the release library
+  // (no gain for this kernel, profiles/r05/r05zr_c3_bench_diag.txt); diag NFN_TILE_ROT_G
+  const int64_t rot = diag_tile_rot_g(a) % ustep;
   issue(u0);
   // an (empty) store behind the first prefetch too: every path into the loop then
   // ends [loads][store] and the hand-off waits with vmcnt(1), not vmcnt(0)

@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(64) chain_grad_kernel(GradArgs ga) {
   float* tile = lds;          // R rows x S
   float* zh = lds + R * S;    // flow inputs: zh[(k * d + j) * R + lane]
   const int lane = threadIdx.x;
-  const int64_t b0 = a.ablate_loads ? 0 : (int64_t)blockIdx.x * R;
+  const int64_t b0 = diag_ablate_loads(a) ? 0 : (int64_t)blockIdx.x * R;
   const int nr = (int)min((int64_t)R, a.B - b0);
   const bool tb = a.t_rowstride == 0;
   if (a.P > 0) stage_rows(tile, a.t + (tb ? 0 : b0 * a.t_rowstride), a.t_rowstride, nr, a.P, S, a.vec4 != 0);
@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
   float gbuf = 1.0f;
   bool issued_once = false;
   auto issue = [&](int64_t tile) {
-    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    if (diag_ablate_loads(a) && issued_once) return;  // diagnostic: compute-only timing
     issued_once = true;
     const int64_t b0 = tile * 64;
     const int nr = (int)min((int64_t)64, a.B - b0);
@@ -130,8 +130,9 @@ __global__ void __launch_bounds__(kMaxBlock, MINW) chain_grad_wave_kernel(GradAr
   };
 
   const int64_t ntiles = a.ntiles;
-  // rotated tile slots (a.tile_rot: chain_wave1_kernel's walk; 0 = the plain grid stride)
-  const int64_t rot = a.tile_rot % ustep;
+  // rotated tile slots as in chain_wave1_kernel: the plain grid stride (rot = 0) in the release
+  // library (the rotation loses 0.8 % here, profiles/r05/r05zx_grad_bench_diag.txt); diag NFN_TILE_ROT_B
+  const int64_t rot = diag_tile_rot_b(a) % ustep;
   if (u0 < ntiles) issue(u0);
   for (int64_t tile = u0, base = 0, slot = u0, tnext; tile < ntiles; tile = tnext) {
     slot += rot;
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_wave1_kernel(GradArgs ga
   const bool has_g = ga.g_out != nullptr;
   const bool want_lp = a.out != nullptr;
   const uint32_t types = a.prog.types[0];
-  const int64_t abl_tile = a.ablate_loads ? u0 : -1;  // diagnostic: compute-only timing
+  const int64_t abl_tile = diag_ablate_loads(a) ? u0 : -1;  // diagnostic: compute-only timing
   // loop-invariant byte offsets (the host guarantees 64 rows of a tile span < 2 GiB)
   const int yoff = lane * (int)a.y_bstride * 4;
   const int toff = (r0 * (int)rs + 4 * c4) * 4;
@@ -370,7 +371,7 @@ __global__ void __launch_bounds__(kMaxBlock, 4) chain_grad_pc_kernel(GradArgs ga
   const int yoff = lane * (int)a.y_bstride * 4;
   const int toff = (r0 * (int)rs + 4 * c4) * 4;
   const int kstep = RSTEP * (int)rs * 4;
-  const int64_t abl_unit = a.ablate_loads ? (int64_t)blockIdx.x : -1;  // diagnostic: compute-only timing
+  const int64_t abl_unit = diag_ablate_loads(a) ? (int64_t)blockIdx.x : -1;  // diagnostic: compute-only timing
   if (wid == 0) {
     // ---- streamer ----
     float4 buf[C][Q];

@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group_kernel(GradArgs ga
   float gbuf = 1.0f;
   bool issued_once = false;
   auto issue = [&](int64_t tile) {
-    if (a.ablate_loads && issued_once) return;  // diagnostic: compute-only timing
+    if (diag_ablate_loads(a) && issued_once) return;  // diagnostic: compute-only timing
     issued_once = true;
     const int64_t b0 = tile * R;
     const int nr = (int)min((int64_t)R, a.B - b0);
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_grad_group1_kernel(GradArgs g
     ymean[i] = (norm && jj < d) ? a.y_mean[jj] : 0.0f;
     ystd[i] = (norm && jj < d) ? a.y_std[jj] : 1.0f;
   }
-  const int abl = a.ablate_loads;
+  const bool abl = diag_ablate_loads(a);
   float4 buf[NV];
   float ybuf[DPL];
   float gbuf;

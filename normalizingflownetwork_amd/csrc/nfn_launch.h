@@ -27,6 +27,17 @@ struct LaunchEvents {
 };
 LaunchEvents& launch_events();
 
+// The measurement hook belongs to the very next API call: that call's first launch takes
+// it, and whatever the call does (a validation error, B == 0, a memset-only path) the hook
+// is disarmed when it returns, so it never times an unrelated later call.  Every extern "C"
+// entry point that can launch holds one.
+struct HookScope {
+  HookScope() = default;
+  HookScope(const HookScope&) = delete;
+  HookScope& operator=(const HookScope&) = delete;
+  ~HookScope() { launch_events() = LaunchEvents{}; }
+};
+
 // Every kernel launch of the library: a plain launch, or — when the caller armed the
 // measurement hook — hipExtLaunchKernel with the pending events (the dispatch's own
 // timestamps), after which the hook clears.
@@ -167,12 +178,6 @@ void launch_flow_vjp(bool fast, int dm, const FlowVjpArgs& v, hipStream_t s);
 // wave-owned persistent form; false if (dm, nv) has no instance
 bool launch_grad_wave(bool fast, int dm, int nv, const GradArgs& ga, size_t lds_block, int waves_per_block,
                       hipStream_t s, int64_t* grid);
-#ifdef NFN_DIAG
-// nfn_grad2.hip (diag A/B; the unit is empty outside NFN_DIAG builds): d = 1 fast-math
-// backward with two samples per lane (128-row wave tiles), P = 4Q with Q in {2, 4, 8};
-// false for other Q
-bool launch_grad_wave2(int Q, const GradArgs& ga, hipStream_t s, int64_t* grid);
-#endif
 // nfn_grad_group.hip (compiled once per math mode); false if (G, DPL, nv) has no instance
 bool launch_grad_group_fast(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s, int64_t* grid);
 bool launch_grad_group_precise(int G, int DPL, int nv, const GradArgs& ga, size_t lds, hipStream_t s,

@@ -140,3 +140,25 @@ void launch_posterior_merge(bool fast, const float2* parts, int nsplit, int S, i
 }
 
 }  // namespace nfn
+
+#ifdef NFN_DIAG
+// Diagnostic build only (not in include/nfn.h): tanh_fast — the planar flows' tanh in every
+// fast-math kernel — over n points, so tests/diag_modes.py can pin its ulp bound on the
+// device against fp64.
+namespace nfn {
+namespace {
+__global__ void __launch_bounds__(256) tanh_fast_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = tanh_fast(x[i]);
+}
+}  // namespace
+}  // namespace nfn
+
+extern "C" int32_t nfn_diag_tanh_fast(const float* x, float* y, int64_t n, void* stream) {
+  const nfn::HookScope hook_scope;
+  if (n <= 0) return NFN_OK;
+  nfn::nfn_launch(nfn::tanh_fast_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                  reinterpret_cast<hipStream_t>(stream), x, y, n);
+  return hipGetLastError() == hipSuccess ? NFN_OK : NFN_E_HIP;
+}
+#endif

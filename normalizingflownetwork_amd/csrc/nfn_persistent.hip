@@ -24,13 +24,13 @@ auto posterior_hpair_kernel(int sel) {
   }
 }
 
-template <int Q, int U = 1, bool SPLIT = false>
+template <int Q, int U = 1>
 auto wave1_hpair_kernel(int sel) {
   switch (sel) {
-    case 0: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 0, U), false, SPLIT>;
-    case 1: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 1, U), false, SPLIT>;
-    case 3: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 0, U), false, SPLIT>;
-    default: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 1, U), false, SPLIT>;
+    case 0: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 0, U)>;
+    case 1: return chain_wave1_kernel<true, Q, true, false, hpair_form(0, 1, U)>;
+    case 3: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 0, U)>;
+    default: return chain_wave1_kernel<true, Q, true, false, hpair_form(1, 1, U)>;
   }
 }
 #endif
@@ -58,14 +58,6 @@ void launch_w1(const ChainArgs& a, int T, size_t lds, hipStream_t s, int64_t* gr
     kfn = chain_wave1_kernel<true, Q, true, false, kStaticProg>;
   if (cm == kChainHPair && hpair_types(a) >= 0)
     kfn = env_int("NFN_HPAIR_U", 1) == 0 ? wave1_hpair_kernel<Q, 0>(hpair_types(a)) : wave1_hpair_kernel<Q>(hpair_types(a));
-  // split issue (A/B): the next tile's rows in two halves, the second after half of the pairs
-  if (a.split_issue == 1 && hpair_types(a) >= 0) kfn = wave1_hpair_kernel<Q, 1, true>(hpair_types(a));
-  // LDS-DMA row fill (A/B): two LDS slots per wave, d = 1 packed loop form
-  if (env_int("NFN_WAVE1_DMA", 0) == 1 && Q <= 8 && a.prog.K <= 16) {
-    kfn = a.prog.K <= kPairsMaxKStream ? chain_wave1_kernel<true, Q, true, false, kChainPairs, true>
-                                       : chain_wave1_kernel<true, Q, true, false, kChainLoop, true>;
-    lds = 2 * (lds - 16) + 16;
-  }
 #endif
 #endif
   const int64_t units = a.ntiles;

@@ -141,8 +141,12 @@ class FlowDistribution:
         so the reference has no such window).  From then on the Chain keeps its snapshot."""
         if self._bijector is None:
             d = self._n_dims
-            flow_t = _cols(self._t, 2 * d, _shape(self._t)[-1]) if self._trainable else self._t
-            self._bijector = Invert(InverseNormalizingFlowLayer._get_bijector(flow_t, self._flow_types, d))
+            # built under grad mode whenever t requires grad: a Chain first touched under
+            # torch.no_grad() (sampling) is cached, and later forward / fldj calls must still
+            # differentiate into t (ADVICE r05)
+            with torch.set_grad_enabled(isinstance(self._t, torch.Tensor) and self._t.requires_grad):
+                flow_t = _cols(self._t, 2 * d, _shape(self._t)[-1]) if self._trainable else self._t
+                self._bijector = Invert(InverseNormalizingFlowLayer._get_bijector(flow_t, self._flow_types, d))
         return self._bijector
 
     @property

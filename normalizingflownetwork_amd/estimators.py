@@ -357,12 +357,13 @@ class BaseEstimator:
                         side = torch.cuda.Stream(device=dev)
                         side.wait_stream(torch.cuda.current_stream(dev))
                         g_ = torch.cuda.CUDAGraph()
+                        mark = ops.graph_pin_mark()
                         with torch.cuda.stream(side):
                             with torch.cuda.graph(g_, stream=side):
                                 step(sidx, snx, sny)
                         torch.cuda.current_stream(dev).wait_stream(side)
                         # the workspaces the capture pinned live exactly as long as this graph
-                        graph = (g_, sidx, snx, sny, ops.take_graph_workspaces(side))
+                        graph = (g_, sidx, snx, sny, ops.take_graph_workspaces(side, mark))
                         g_.replay()
                         continue
                     opt.zero_grad(set_to_none=True)

@@ -43,14 +43,19 @@ def snapshot_rows(t):
     as the layer's base columns pad the wide ``t`` (C2: 2 + 30 = 32 floats); a row's first
     flow column itself sits ``lead`` floats after that boundary.  A broadcast row (stride 0)
     stays one row.  Numpy / list inputs pass through (each flow moves its own slice:
-    already a copy).  When ``t`` requires grad (and grad mode is on) the copy is an autograd
-    op, so gradients of the flows' outputs reach ``t`` as TF's tape reaches the Dense output.
+    already a copy).  When ``t`` requires grad the copy is an autograd op WHATEVER the grad
+    mode at the time (a bijector first built under ``torch.no_grad()``, e.g. while sampling,
+    is cached and later differentiated), so gradients of the flows' outputs reach ``t`` as
+    TF's tape reaches the Dense output.
     Memory: the snapshot holds B x (W + lead) floats (C2's 2^24 x 32: 2 GiB) until the flows
     built on it are dropped."""
     if not isinstance(t, torch.Tensor) or t.dim() != 2:
         return t
-    if not (torch.is_grad_enabled() and t.requires_grad):
-        t = t.detach()
+    with torch.set_grad_enabled(t.requires_grad):
+        return _snapshot(t)
+
+
+def _snapshot(t: torch.Tensor) -> torch.Tensor:
     B, W = int(t.shape[0]), int(t.shape[1])
     if B > 1 and t.stride(0) == 0:
         return t[:1].clone().expand(B, W)

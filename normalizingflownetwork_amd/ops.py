@@ -75,22 +75,46 @@ _ws_lock = threading.Lock()
 # this (pooled / side streams come and go: fit's capture stream, the bench's ring).
 WORKSPACE_CACHE_ENTRIES = 8
 # Workspaces a captured HIP graph may hold the address of: handed out while their stream
-# was capturing, as ((device, stream) key, workspace).  A graph's replays write partials and
-# the ticket there, so the block must not go back to the allocator while the graph lives.
-# Graphs do not tell when they die: an entry stays pinned for the life of the process unless
-# the capturing code takes it over (``take_graph_workspaces``) and keeps it next to its graph,
-# as ``estimators.fit`` does.
+# was capturing, as (pin sequence number, (device, stream) key, workspace).  A graph's replays
+# write partials and the ticket there, so the block must not go back to the allocator while
+# the graph lives.  Graphs do not tell when they die: an entry stays pinned for the life of
+# the process unless the capturing code takes it over (``graph_pin_mark`` before the capture,
+# ``take_graph_workspaces`` after it) and keeps it next to its graph, as ``estimators.fit``
+# does.  Stream handles are pooled and reused, so a take is scoped by the mark, not only by
+# the stream: pins made before the mark (another live graph's) stay where they are.
 _graph_workspaces: list = []
+_pin_seq = 0
 
 
-def take_graph_workspaces(stream) -> list:
-    """Unpin and return the workspaces pinned by captures on ``stream`` (a torch stream):
-    the caller keeps them alive exactly as long as the graph(s) captured there."""
+def graph_pin_mark() -> int:
+    """The pin sequence number before a capture: ``take_graph_workspaces(stream, mark)`` then
+    hands back exactly the workspaces that capture pinned."""
+    with _ws_lock:
+        return _pin_seq
+
+
+def take_graph_workspaces(stream, since: int) -> list:
+    """Unpin and return the workspaces pinned on ``stream`` (a torch stream) since ``since``
+    (a ``graph_pin_mark()``): the caller keeps them alive exactly as long as the graph
+    captured there.  Pins made before the mark, on this stream handle or any other, stay."""
     key = (stream.device.index, int(stream.cuda_stream))
     with _ws_lock:
-        mine = [ws for k, ws in _graph_workspaces if k == key]
-        _graph_workspaces[:] = [(k, ws) for k, ws in _graph_workspaces if k != key]
+        return _take_pins(key, since)
+
+
+def _take_pins(key, since: int) -> list:
+    mine = [ws for seq, k, ws in _graph_workspaces if k == key and seq >= since]
+    _graph_workspaces[:] = [(seq, k, ws) for seq, k, ws in _graph_workspaces if not (k == key and seq >= since)]
     return mine
+
+
+def _pin(key, ws) -> None:
+    """Pin ``ws`` for a capture on ``key`` (caller holds ``_ws_lock``).  A block already pinned
+    by an earlier capture that nobody took stays pinned for the process: not pinned again."""
+    global _pin_seq
+    if not any(p is ws for _, _, p in _graph_workspaces):
+        _graph_workspaces.append((_pin_seq, key, ws))
+        _pin_seq += 1
 
 
 def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
@@ -109,8 +133,8 @@ def _workspace(n_doubles: int, device: torch.device) -> torch.Tensor:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < n_doubles:
             ws = torch.empty(max(2, n_doubles), dtype=torch.float64, device=device)
-        if capturing and not any(p is ws for _, p in _graph_workspaces):
-            _graph_workspaces.append((key, ws))
+        if capturing:
+            _pin(key, ws)
         _workspaces[key] = ws
         _workspaces.move_to_end(key)
         while len(_workspaces) > WORKSPACE_CACHE_ENTRIES:

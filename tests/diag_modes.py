@@ -65,38 +65,27 @@ def strategies():
         os.environ.pop("NFN_POST_SPLIT")
     np.testing.assert_allclose(out.cpu().numpy(), out1.cpu().numpy(), rtol=2e-6, atol=2e-6)
     res["post_split_vs_single"] = "allclose 2e-6"
-    # C2 shape on chain_wave1_kernel (ragged tail): the hand-off issue orders under study give
-    # the default order's values bitwise (the same pair bodies on the same rows)
+    # C2 shape on chain_wave1_kernel (ragged tail): the plain tile walk (diag NFN_TILE_ROT=0)
+    # gives the rotated walk's per-sample values bitwise (the same math on the same rows) and
+    # the same fixed-order fp64 sum
     B2 = (1 << 20) + 37
     y2 = torch.randn((B2, 1), generator=gen, device="cuda")
     t2 = torch.randn((B2, 32), generator=gen, device="cuda")
-    base, _ = ops.chain_log_prob(y2, t2, ft, 1, True)
-    for knob in ("NFN_SPLIT_ISSUE", "NFN_EARLY_ISSUE", "NFN_XCD_SKEW"):
-        os.environ[knob] = "6" if knob == "NFN_XCD_SKEW" else "1"
-        try:
-            got, _ = ops.chain_log_prob(y2, t2, ft, 1, True)
-        finally:
-            os.environ.pop(knob)
-        assert torch.equal(got, base), knob
-        res[knob.lower()] = "bitwise"
-    # the XCD-skewed last steps need whole steps: B = 2^20 (8 steps of the 2048-wave grid)
-    y3, t3 = y2[: 1 << 20], t2[: 1 << 20]
-    base3, s3 = ops.chain_log_prob(y3, t3, ft, 1, True, want_sum=True)
-    os.environ["NFN_XCD_SKEW"] = "6"
+    base, s2 = ops.chain_log_prob(y2, t2, ft, 1, True, want_sum=True)
+    os.environ["NFN_TILE_ROT"] = "0"
     try:
-        got3, g3 = ops.chain_log_prob(y3, t3, ft, 1, True, want_sum=True)
+        got, g2 = ops.chain_log_prob(y2, t2, ft, 1, True, want_sum=True)
     finally:
-        os.environ.pop("NFN_XCD_SKEW")
-    assert torch.equal(got3, base3), "NFN_XCD_SKEW whole steps"
-    assert abs(float(g3.item()) - float(s3.item())) <= 1e-12 * abs(float(s3.item()))
-    res["nfn_xcd_skew_whole_steps"] = "bitwise"
+        os.environ.pop("NFN_TILE_ROT")
+    assert torch.equal(got, base), "NFN_TILE_ROT=0"
+    assert abs(float(g2.item()) - float(s2.item())) <= 1e-12 * abs(float(s2.item()))
+    res["nfn_tile_rot_0"] = "bitwise"
     res["library"] = os.path.basename(_lib.LIB_PATH)
     return res
 
 
 def grad_stream():
-    """d = 1 backward: the two-samples-per-lane kernel (chain_grad_wave2_kernel, diag
-    NFN_GRAD_WAVE2=1), the straight-line buffer pipeline (chain_grad_wave1_kernel, diag
+    """d = 1 backward: the straight-line buffer pipeline (chain_grad_wave1_kernel, diag
     NFN_GRAD_WAVE1=1, in one or two prefetch pieces) and the producer / consumer workgroup
     (chain_grad_pc_kernel, NFN_GRAD_PC=1) against the release's wave kernel
     (chain_grad_wave_kernel): the same per-sample math, so log_prob, d/dt and d/dy must be
@@ -119,17 +108,17 @@ def grad_stream():
         g = torch.randn((B,), generator=gen, device="cuda")
         ym, ys = (np.float32([norm[0]]), np.float32([norm[1]])) if norm else (None, None)
         outs = {}
-        for v, split, pc, w2 in (("0", "1", "0", "0"), ("1", "1", "0", "0"), ("1", "2", "0", "0"),
-                                 ("0", "1", "1", "0"), ("0", "1", "0", "1")):
+        for v, split, pc, rot in (("0", "1", "0", "0"), ("1", "1", "0", "0"), ("1", "2", "0", "0"),
+                                  ("0", "1", "1", "0"), ("0", "1", "0", "4")):
             os.environ["NFN_GRAD_WAVE1"], os.environ["NFN_GRAD_SPLIT"], os.environ["NFN_GRAD_PC"] = v, split, pc
-            os.environ["NFN_GRAD_WAVE2"] = w2
+            os.environ["NFN_TILE_ROT_B"] = rot
             try:
-                outs[v + split + pc + w2] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
+                outs[v + split + pc + rot] = ops.chain_log_prob_grad(y, t, ft, 1, True, ym, ys, g_out=g, want_logp=True)
             finally:
-                for k in ("NFN_GRAD_WAVE1", "NFN_GRAD_SPLIT", "NFN_GRAD_PC", "NFN_GRAD_WAVE2"):
+                for k in ("NFN_GRAD_WAVE1", "NFN_GRAD_SPLIT", "NFN_GRAD_PC", "NFN_TILE_ROT_B"):
                     os.environ.pop(k)
         outs["01"] = outs["0100"]
-        for alt in ("1100", "1200", "0110", "0101"):
+        for alt in ("1100", "1200", "0110", "0104"):
             for a, b, what in zip(outs[alt], outs["01"], ("log_prob", "grad_t", "grad_y")):
                 same = (a == b) | (torch.isnan(a) & torch.isnan(b))
                 assert bool(same.all()), f"{ft} B={B} {alt} {what}: {int((~same).sum())} values differ"
@@ -214,6 +203,37 @@ def flow_tile():
     return res
 
 
+def tanh():
+    """tanh_fast (the planar flows' tanh in every fast-math kernel) on the device against fp64
+    over a dense sweep of [-1, 1] (where the two branches meet, at |a| = 0.3) and a coarser one
+    of [-12, 12]: the largest error in fp32 ulps of the correctly rounded result.  The bound
+    is pinned by test_gpu_diag, so a change cannot loosen it silently."""
+    import ctypes
+
+    import torch
+
+    from normalizingflownetwork_amd import build
+
+    lib = ctypes.CDLL(build.DIAG_OUT)
+    fn = lib.nfn_diag_tanh_fast
+    fn.restype, fn.argtypes = ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    res = {"library": os.path.basename(build.DIAG_OUT)}
+    for name, lo, hi, n in (("sweep_1", -1.0, 1.0, 1 << 22), ("sweep_12", -12.0, 12.0, 1 << 22)):
+        x = np.linspace(lo, hi, n, dtype=np.float32)
+        x = x[x != 0.0]
+        xd = torch.from_numpy(x).cuda()
+        yd = torch.empty_like(xd)
+        assert fn(xd.data_ptr(), yd.data_ptr(), xd.numel(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        got = yd.cpu().numpy()
+        ref = np.tanh(x.astype(np.float64))
+        ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
+        err = np.abs(got.astype(np.float64) - ref) / ulp
+        k = int(np.argmax(err))
+        res[name] = {"max_ulp": float(err.max()), "at": float(x[k]), "mean_ulp": float(err.mean())}
+    return res
+
+
 def release():
     from normalizingflownetwork_amd import _lib, ops
 
@@ -240,4 +260,4 @@ def release():
 if __name__ == "__main__":
     which = sys.argv[1]
     print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream, "flow_tile": flow_tile,
-                             "densep": densep}[which]()}), flush=True)
+                             "densep": densep, "tanh": tanh}[which]()}), flush=True)

@@ -153,3 +153,31 @@ def test_no_grad_keeps_the_one_launch_chain(gpu):
     np.testing.assert_allclose(l1.detach().cpu().numpy(), l0.cpu().numpy(), rtol=1e-5, atol=1e-5)
     with torch.no_grad():
         assert chain._fused(y_req) is not None
+
+
+def test_bijector_first_built_under_no_grad_still_differentiates(gpu):
+    """``dist.bijector`` caches its Chain (and the parameter snapshot) on FIRST access.  When
+    that access happens under ``torch.no_grad()`` (e.g. while sampling), later grad-enabled
+    forward / fldj calls must still reach ``t`` — as TF's tape would: the same
+    gradients as a bijector built with grad mode on."""
+    from normalizingflownetwork_amd import InverseNormalizingFlowLayer
+
+    fx = load_golden("asym_pra_d3")
+    ft, d, tr = fx["flow_types"], fx["d"], bool(fx["trainable"])
+    y, t = fx["y"][:256].astype(np.float32), fx["t"][:256].astype(np.float32)
+    layer = InverseNormalizingFlowLayer(ft, d, tr)
+    grads = []
+    for first_no_grad in (False, True):
+        tt = torch.tensor(t, device=gpu, requires_grad=True)
+        dist = layer(tt)
+        if first_no_grad:
+            with torch.no_grad():
+                chain = dist.bijector.bijector
+                chain.forward_and_log_det_jacobian(torch.tensor(y, device=gpu))  # sampling-like use
+        else:
+            chain = dist.bijector.bijector
+        x, ldj = chain.forward_and_log_det_jacobian(torch.tensor(y, device=gpu))
+        assert ldj.requires_grad, "the cached Chain lost its graph to t"
+        (x.sum() + ldj.sum()).backward()
+        grads.append(tt.grad.cpu().numpy())
+    np.testing.assert_array_equal(grads[1], grads[0])

@@ -419,7 +419,7 @@ def test_graph_workspace_survives_cache_eviction(gpu):
         _, s_graph = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
     (key,) = [k for k in ops._workspaces if k[1] == int(side.cuda_stream)]
     ws = ops._workspaces[key]
-    assert any(p is ws for _, p in ops._graph_workspaces)
+    assert any(p is ws for _, _, p in ops._graph_workspaces)
     streams = [torch.cuda.Stream() for _ in range(ops.WORKSPACE_CACHE_ENTRIES + 2)]
     for st in streams:
         with torch.cuda.stream(st):
@@ -453,9 +453,10 @@ def test_taken_graph_workspaces_are_unpinned(gpu):
         with torch.cuda.stream(side):
             ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
         g = torch.cuda.CUDAGraph()
+        mark = ops.graph_pin_mark()
         with torch.cuda.graph(g, stream=side):
             _, s_graph = ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)
-        mine = ops.take_graph_workspaces(side)
+        mine = ops.take_graph_workspaces(side, mark)
         assert len(mine) == 1
         kept.append((g, s_graph, mine))
         assert len(ops._graph_workspaces) == n0
@@ -464,4 +465,44 @@ def test_taken_graph_workspaces_are_unpinned(gpu):
     torch.cuda.synchronize()
     ref = float(ops.chain_log_prob(y, t, ft, d, True, want_values=False, want_sum=True)[1][0].item())
     for _, s_graph, _ in kept:
+        assert float(s_graph[0].item()) == pytest.approx(ref, rel=1e-12)
+
+
+def test_take_leaves_another_graphs_pin_on_the_same_stream(gpu):
+    """Two graphs captured on ONE stream handle (torch pools and reuses stream handles):
+    the first is left pinned process-wide, the second is captured between a pin mark and a
+    take.  The take hands back only what the second capture pinned (here a larger block,
+    since it outgrew the first's), the first graph's block stays pinned, and both graphs
+    still replay correctly after the cache has evicted the stream's entry."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d = ("planar", "radial") * 5, 1
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    y = torch.randn((1 << 20, 1), generator=gen, device="cuda")
+    t = torch.randn((1 << 20, 32), generator=gen, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graphs = []
+    for B in (10_000, 1 << 20):  # the second needs more partials: a new, larger workspace
+        with torch.cuda.stream(side):
+            ops.chain_log_prob(y[:B], t[:B], ft, d, True, want_values=False, want_sum=True)
+        g = torch.cuda.CUDAGraph()
+        mark = ops.graph_pin_mark()
+        with torch.cuda.graph(g, stream=side):
+            _, s_graph = ops.chain_log_prob(y[:B], t[:B], ft, d, True, want_values=False, want_sum=True)
+        key = (side.device.index, int(side.cuda_stream))
+        graphs.append((B, g, s_graph, ops._workspaces[key], mark))
+    (_, _, _, ws_a, _), (_, _, _, ws_b, mark_b) = graphs
+    assert ws_a is not ws_b
+    mine = ops.take_graph_workspaces(side, mark_b)
+    assert len(mine) == 1 and mine[0] is ws_b
+    assert any(p is ws_a for _, _, p in ops._graph_workspaces), "the first graph's block was unpinned"
+    for st in [torch.cuda.Stream() for _ in range(ops.WORKSPACE_CACHE_ENTRIES + 2)]:
+        with torch.cuda.stream(st):
+            ops.chain_log_prob(y[:1000], t[:1000], ft, d, True, want_values=False, want_sum=True)
+    torch.cuda.synchronize()
+    for B, g, s_graph, _, _ in graphs:
+        g.replay()
+        torch.cuda.synchronize()
+        ref = float(ops.chain_log_prob(y[:B], t[:B], ft, d, True, want_values=False, want_sum=True)[1][0].item())
         assert float(s_graph[0].item()) == pytest.approx(ref, rel=1e-12)

@@ -114,6 +114,13 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_sq2_dgrad 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_sq2_dgrad" -o s2 -- \
         python3 "$ROOT/bench.py" --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_sq_dgrad_sb)  # the fused Dense backward, f32 vs split-bf16 GEMMs (diag NFN_DGRAD_SB): two SQ passes each
+      for v in 0 1; do
+        { cd /tmp; NFN_DGRAD_SB=$v run pmc_sq1_dgrad_sb$v 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace --output-format csv -d "$OUT/pmc_sq1_dgrad_sb$v" -o s1 -- \
+          python3 "$ROOT/bench.py" --diag --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+        { cd /tmp; NFN_DGRAD_SB=$v run pmc_sq2_dgrad_sb$v 90 timeout -s KILL 80 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_LDS --kernel-trace --output-format csv -d "$OUT/pmc_sq2_dgrad_sb$v" -o s2 -- \
+          python3 "$ROOT/bench.py" --diag --mode dense_grad --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
+      done ;;
     pmc_sq_fwd)  # issue / stall breakdown of the C5 posterior and the C2 forward (two counter passes each)
       for cfg in C5 C2; do
         { cd /tmp; run pmc_sq1_$cfg 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d "$OUT/pmc_sq1_$cfg" -o s1 -- \
@@ -138,15 +145,6 @@ for s in $STEPS; do
         for c in FETCH_SIZE WRITE_SIZE; do
           { cd /tmp; run pmc_all_${i}_$c 100 timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_all_${i}_$c" -o p -- \
             python3 "$ROOT/bench.py" $args --steps 5 --warmup 2 --prewarm-ms 0 --no-cpu-baseline; cd "$ROOT"; }
-        done
-      done ;;
-    pmc_dma)  # C2 forward, register hand-off vs LDS-DMA row fill (diag build): HBM bytes + SQ counters per variant
-      for v in regs dma; do
-        if [ $v = dma ]; then K=NFN_WAVE1_DMA=1; else K=NFN_WAVE1_DMA=0; fi
-        for c in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" "SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA"; do
-          tag=$(echo $c | cut -d' ' -f1)
-          { cd /tmp; run pmc_dma_${v}_$tag 100 timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$OUT/pmc_dma_${v}_$tag" -o p -- \
-            python3 "$ROOT/tools/run_variant.py" C2 $K --launches 5; cd "$ROOT"; }
         done
       done ;;
     pmc_lds)  # LDS bank-conflict cycles of every bench kernel (one counter pass per mode)

@@ -357,5 +357,103 @@ def make_planar_m_exact(tanh=tanh_t3):
 FORMS["m_exact"] = (make_planar_m_exact(), radial_r3, base_r3)
 
 
+# Round 6 (verdict r05 "Next" 3): a cancellation-aware m near w u = log(e - 1), where
+# softplus(w u) - 1 cancels.  With delta = w u - log(e - 1) formed by one fma against the
+# two-float constant X0H + X0L (the product w u is exact inside the fma: no rounding of w u
+# enters delta), m = log1p((1 - 1/e) expm1(delta)) + 1e-5 = delta P(delta) + 1e-5 with a
+# degree-5 polynomial fitted for relative error on |delta| <= 0.25 (<= 2 ulp in fp32 Horner);
+# outside that range the existing form (softplus - (1 - 1e-5)) is not cancellation-limited.
+X0H, X0L = F(0.54132485), F(7.158233e-10)
+M_POLY = [F(0.63212055), F(0.11627208), F(-0.010241115), F(-0.0038298753), F(0.0009094632), F(0.00016557719)]
+M_RANGE = F(0.25)
+
+
+def m_delta(w, u, sp):
+    d = fma(w, u, -X0H) - X0L
+    p = M_POLY[5]
+    for c in M_POLY[4::-1]:
+        p = fma(d, p, c)
+    md = fma(d, p, F(1e-5))
+    return np.where(np.abs(d) <= M_RANGE, md, sp - ONE_M)
+
+
+def make_planar_mdelta(tanh=tanh_t3):
+    def planar(z, u, wraw, b):
+        w = wraw + F(1)
+        wtu = w * u
+        nw2 = fma(w, w, F(1e-9))
+        rn = rcp(nw2)
+        sp = softplus_alpha(wtu)
+        m = m_delta(w, u, sp)
+        uh = fma(u, F(1e-9), m * w) * rn
+        qd = fma((wtu - m) * F(1e-9), rn, sp + F(1e-5))
+        th = tanh(fma(w, z, b))
+        z = fma(uh, th, z)
+        return z, fma(th, th, fma(-th, th, F(1)) * qd)
+    return planar
+
+
+def make_planar_dfsp(tanh=tanh_t3):
+    """The double-float alternative, emulated at its best: m from a correctly rounded softplus of
+    the EXACT w u (fp64 evaluation) — the floor any double-float softplus could reach."""
+    def planar(z, u, wraw, b):
+        w = wraw + F(1)
+        wtu = w * u
+        wtu64 = np.asarray(w, np.float64) * np.asarray(u, np.float64)
+        sp64 = np.logaddexp(0.0, wtu64)
+        m = r32(sp64 - (1.0 - 1e-5))
+        sp = r32(sp64)
+        nw2 = fma(w, w, F(1e-9))
+        rn = rcp(nw2)
+        uh = fma(u, F(1e-9), m * w) * rn
+        qd = fma((wtu - m) * F(1e-9), rn, sp + F(1e-5))
+        th = tanh(fma(w, z, b))
+        z = fma(uh, th, z)
+        return z, fma(th, th, fma(-th, th, F(1)) * qd)
+    return planar
+
+
+FORMS["mdelta"] = (make_planar_mdelta(), radial_r3, base_r3)
+FORMS["dfsp"] = (make_planar_dfsp(), radial_r3, base_r3)
+
+
+def fit_m_poly(R, deg):
+    """fp32 coefficients of P with log1p((1 - 1/e) expm1(d)) ~= d P(d) on |d| <= R (relative
+    least squares on Chebyshev nodes)."""
+    c = 1 - 1 / np.e
+    d = np.cos(np.linspace(0, np.pi, 8001)) * R
+    d = d[np.abs(d) > 1e-12]
+    g = np.log1p(c * np.expm1(d)) / d
+    V = np.vander(d, deg + 1, increasing=True)
+    coef, *_ = np.linalg.lstsq(V / g[:, None], np.ones_like(g), rcond=None)
+    return [F(x) for x in coef]
+
+
+def make_planar_mdelta_r(R, deg, tanh=tanh_t3):
+    cf, RR = fit_m_poly(R, deg), F(R)
+
+    def planar(z, u, wraw, b):
+        w = wraw + F(1)
+        wtu = w * u
+        nw2 = fma(w, w, F(1e-9))
+        rn = rcp(nw2)
+        sp = softplus_alpha(wtu)
+        d = fma(w, u, -X0H) - X0L
+        p = cf[-1]
+        for c in cf[-2::-1]:
+            p = fma(d, p, c)
+        m = np.where(np.abs(d) <= RR, fma(d, p, F(1e-5)), sp - ONE_M)
+        uh = fma(u, F(1e-9), m * w) * rn
+        qd = fma((wtu - m) * F(1e-9), rn, sp + F(1e-5))
+        th = tanh(fma(w, z, b))
+        z = fma(uh, th, z)
+        return z, fma(th, th, fma(-th, th, F(1)) * qd)
+    return planar
+
+
+for _R, _deg in ((0.75, 7), (1.5, 11), (2.0, 13), (3.0, 17)):
+    FORMS[f"md{_R}"] = (make_planar_mdelta_r(_R, _deg), radial_r3, base_r3)
+
+
 if __name__ == "__main__":
     main()

@@ -613,19 +613,6 @@ def main():
             run_grad(cfg, [{"name": "full", "env": {}}, {"name": "memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
                            {"name": "compute_only", "env": {"NFN_ABLATE_LOADS": 1}}], rounds=4)
         return
-    if which[0] == "grad2":  # d = 1 backward: two samples per lane (wave2, 128-row tiles, diag) vs one (wave)
-        W2 = {"NFN_GRAD_WAVE2": 1}
-        for cfg in ("C2", "R2"):
-            run_grad(cfg, [{"name": "wave", "env": {}}, {"name": "wave2", "env": dict(W2)},
-                           {"name": "wave_memory_only", "env": {"NFN_ABLATE_FLOWS": 1}},
-                           {"name": "wave2_memory_only", "env": dict(W2, NFN_ABLATE_FLOWS=1)},
-                           {"name": "wave_compute_only", "env": {"NFN_ABLATE_LOADS": 1}},
-                           {"name": "wave2_compute_only", "env": dict(W2, NFN_ABLATE_LOADS=1)},
-                           {"name": "wave2_wg2", "env": dict(W2, NFN_WG_PER_CU=2)},
-                           {"name": "wave2_wg2_memory_only", "env": dict(W2, NFN_WG_PER_CU=2, NFN_ABLATE_FLOWS=1)},
-                           {"name": "wave2_noprio", "env": dict(W2, NFN_PRIO=0)},
-                           {"name": "wave_b", "env": {}}, {"name": "wave2_b", "env": dict(W2)}], rounds=4)
-        return
     if which[0] == "gradw1":  # d = 1 backward: straight-line buffer pipeline vs the generic wave kernel
         for cfg in ("C2", "R2"):
             G = {"NFN_GRAD_WAVE1": 0}
@@ -718,13 +705,6 @@ def main():
                            {"name": "tile_per_workgroup", "env": {"NFN_GRAD_WAVE": 0}},
                            {"name": "wave_wpb1", "env": {"NFN_GRAD_WPB": 1}},
                            {"name": "wave_wpb4", "env": {"NFN_GRAD_WPB": 4}}])
-        return
-    if which[0] == "dma":  # C2 forward: register prefetch + ds_write hand-off vs LDS-DMA row fill
-        for cfg in ("C2", "R2"):
-            run(cfg, [{"name": "regs", "env": {}}, {"name": "lds_dma", "env": {"NFN_WAVE1_DMA": 1}},
-                      {"name": "regs_memonly", "env": {"NFN_ABLATE_FLOWS": 1}},
-                      {"name": "lds_dma_memonly", "env": {"NFN_WAVE1_DMA": 1, "NFN_ABLATE_FLOWS": 1}}],
-                rounds=4)
         return
     if which[0] == "ceiling":  # HBM ceilings of plain torch streams over the C2 parameter buffer
         B, P = 1 << 24, 32

@@ -3,8 +3,8 @@
 under a diagnostic-build knob (for rocprofv3 --pmc passes over a single variant: run it as
 the program after `--`).
 
-  python3 tools/run_variant.py C2 NFN_WAVE1_DMA=1 [--launches 5]
-  python3 tools/run_variant.py C2 NFN_GRAD_WAVE2=1 --grad"""
+  python3 tools/run_variant.py C2 NFN_TILE_ROT=0 [--launches 5]
+  python3 tools/run_variant.py C2 NFN_GRAD_WAVE1=1 --grad"""
 
 import os
 import sys
