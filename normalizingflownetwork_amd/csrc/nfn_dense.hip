@@ -126,7 +126,8 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
       const float* row = tl + lane * S;
       float lp;
       if constexpr (DM == 1 && FAST)
-        lp = (a.prog.K <= 16 ? eval_chain1_fast<true>(z[0], row, a) : eval_chain1_fast<false>(z[0], row, a)) - corr;
+        lp = (a.prog.K <= 16 ? eval_chain1_fast<true, 1, kChainLoop, false>(z[0], row, a)
+                             : eval_chain1_fast<false, 1, kChainLoop, false>(z[0], row, a)) - corr;
       else
         lp = eval_chain<DM, FAST>(z, row, a) - corr;
       if (a.out) __builtin_nontemporal_store(lp, a.out + b0 + lane);
@@ -265,8 +266,8 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
       }
     }
     wave_lds_sync();
-    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM>(z0, tl + lane, a)
-                                     : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
+    const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM, false>(z0, tl + lane, a)
+                                     : eval_chain1_fast<false, kCS, kChainLoop, false>(z0, tl + lane, a)) - corr;
     if (lane < nr) {
       acc_sum += (double)lp;
       nfc += nonfinite1(lp);
@@ -410,8 +411,8 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
         }
       }
       wave_lds_sync();
-      const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM>(z0, tl + lane, a)
-                                       : eval_chain1_fast<false, kCS>(z0, tl + lane, a)) - corr;
+      const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM, false>(z0, tl + lane, a)
+                                       : eval_chain1_fast<false, kCS, kChainLoop, false>(z0, tl + lane, a)) - corr;
       lse_push<true>(m, lacc, lp);
       wave_lds_sync();  // this unit's LDS reads done before the next unit's writes
     }

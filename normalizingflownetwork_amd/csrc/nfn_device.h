@@ -512,13 +512,44 @@ __device__ __forceinline__ float planar1_uh(float u, float w, float rn, float m)
   return fmaf(u, 1e-9f, m * w) * rn;
 }
 
+// m = -1 + softplus(w u) + 1e-5 without the cancellation of softplus - 1 near
+// w u = log(e - 1) (where m -> 1e-5 and u_hat ~ m / w carries m's relative error into z):
+// with d = w u - log(e - 1), one fma against the two-float constant (the product w u is exact
+// inside it, so no rounding of w u enters d), m = log1p((1 - 1/e) expm1(d)) + 1e-5
+// = d P(d) + 1e-5, P a degree-7 polynomial fitted for relative error on |d| <= 0.75 (<= 2.1
+// ulp in fp32 Horner); outside that range softplus - (1 - 1e-5) is not cancellation-limited.
+// fp32 emulation of the C2 chain (tools/kernel_emu.py "r6" vs "r5", 2^20 random samples,
+// correctly rounded transcendentals): beyond 3e-6 relative 110 -> 31, beyond 1e-5 4 -> 1
+// (profiles/r06/r06_kernel_emu_m_forms.txt); on the GPU, every sample of C2 / C4 against the
+// fp64 oracle: beyond 1e-5 relative 36 / 317 -> 19 / 138 (profiles/r06/r06g_parity.json).
+// The d = 1 fast-math forwards of log_prob, the posterior, the grid and the Bijector API form
+// m here (planar1_fast<true>, grid1_prepare), so their per-sample values stay bitwise one
+// another's.
+constexpr float kX0H = 0.54132485f, kX0L = 7.158233e-10f;  // log(e - 1) = kX0H + kX0L
+__device__ __forceinline__ float planar1_m(float w, float u, float sp) {
+  const float d = fmaf(w, u, -kX0H) - kX0L;
+  float p = fmaf(d, -5.34155e-06f, -7.2508854e-05f);
+  p = fmaf(d, p, 0.00016604575f);
+  p = fmaf(d, p, 0.00091448176f);
+  p = fmaf(d, p, -0.0038299547f);
+  p = fmaf(d, p, -0.010241022f);
+  p = fmaf(d, p, 0.116272084f);
+  p = fmaf(d, p, 0.63212055f);
+  return fabsf(d) <= 0.75f ? fmaf(d, p, 1e-5f) : sp - (1.0f - 1e-5f);
+}
+
+// ACCM: the cancellation-aware m (planar1_m) — every d = 1 fast-math forward except the
+// compute-bound fused Dense kernels and the backward (ACCM = false: m = softplus - (1 - 1e-5),
+// round 5's form; measured costs of the accurate m there, profiles/r06/r06g_*: fused Dense
+// forward +6 %, backward +1 %; C2 / C4 / C5 streams unchanged)
+template <bool ACCM = true>
 __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, float b) {
   const float w = wraw + 1.0f;
   const float wtu = w * u;
   const float nw2 = fmaf(w, w, 1e-9f);
   const float rn = __builtin_amdgcn_rcpf(nw2);
   const float sp = softplus_alpha<true>(wtu);
-  const float m = sp - (1.0f - 1e-5f);
+  const float m = ACCM ? planar1_m(w, u, sp) : sp - (1.0f - 1e-5f);
   const float uh = planar1_uh(u, w, rn, m);
   const float qd = fmaf((wtu - m) * 1e-9f, rn, sp + 1e-5f);
   const float th = tanh_fast(fmaf(w, z, b));
@@ -563,8 +594,9 @@ __device__ __forceinline__ void read3(float (&v)[3], const float* row, int st) {
 // LDS parameter reads, which for flow k+1 are issued before flow k's math.
 __device__ __forceinline__ int size1(int id) { return id == NFN_FLOW_AFFINE ? 2 : 3; }
 
+template <bool ACCM = true>
 __device__ __forceinline__ float flow1_fast(int id, float& z, const float (&p)[3]) {
-  if (id == NFN_FLOW_PLANAR) return planar1_fast(z, p[0], p[1], p[2]);
+  if (id == NFN_FLOW_PLANAR) return planar1_fast<ACCM>(z, p[0], p[1], p[2]);
   if (id == NFN_FLOW_RADIAL) return radial1_fast(z, p[0], p[1], p[2]);
   return affine1_fast(z, p[0], p[1]);
 }
@@ -576,7 +608,7 @@ __device__ __forceinline__ void read3c(float (&v)[3], const float* row, int off)
   v[2] = row[(off + 2) * ST];
 }
 
-template <int ST = 1>
+template <int ST = 1, bool ACCM = true>
 __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, uint32_t types, int K, int P) {
   float l2 = 0.0f;
   int id = (int)(types & 3u);
@@ -593,7 +625,7 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
       const int offn = max(off - size1(idn), 0);
       float pn[3];
       read3c<ST>(pn, row, offn);
-      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<ACCM>(id, z, pc)));
       id = idn;
       off = offn;
       pc[0] = pn[0];
@@ -605,7 +637,7 @@ __device__ __forceinline__ float chain1_fast_packed(float& z, const float* row, 
 }
 
 // A program fixed at compile time (TYPES, K): straight-line code, no dispatch.
-template <uint32_t TYPES, int K, int ST = 1>
+template <uint32_t TYPES, int K, int ST = 1, bool ACCM = true>
 __device__ __forceinline__ float chain1_fast_static(float& z, const float* row, int P) {
   float l2 = 0.0f;
   int off = P;
@@ -615,7 +647,7 @@ __device__ __forceinline__ float chain1_fast_static(float& z, const float* row, 
     off -= size1(id);
     float pc[3];
     read3c<ST>(pc, row, off);
-    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<ACCM>(id, z, pc)));
   }
   return l2;
 }
@@ -624,11 +656,11 @@ __device__ __forceinline__ float chain1_fast_static(float& z, const float* row, 
 // so the second flow's parameter-only work (softplus, u_hat, alpha, beta) can issue
 // under the first flow's z chain, and the type dispatch runs once per pair.  The
 // next pair's parameters are read (LDS) before the current pair is evaluated.
-template <int IA, int IB>
+template <int IA, int IB, bool ACCM = true>
 __device__ __forceinline__ void flow_pair1(float& z, float& l2, const float (&pa)[3], const float (&pb)[3]) {
-  const float da = flow1_fast(IA, z, pa);
+  const float da = flow1_fast<ACCM>(IA, z, pa);
   l2 += __builtin_amdgcn_logf(fabsf(da));
-  const float db = flow1_fast(IB, z, pb);
+  const float db = flow1_fast<ACCM>(IB, z, pb);
   l2 += __builtin_amdgcn_logf(fabsf(db));
 }
 
@@ -649,7 +681,7 @@ __device__ __forceinline__ void flow_pair1(float& z, float& l2, const float (&pa
 // harmless in-row reads of the padded tile).
 __device__ __forceinline__ int type1(uint32_t types, int k) { return (int)((types >> ((2 * k) & 31)) & 3u); }
 
-template <int ST = 1>
+template <int ST = 1, bool ACCM = true>
 __device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, uint32_t types, int K, int P) {
   float l2 = 0.0f;
   int ia = type1(types, 0), ib = type1(types, 1);
@@ -664,7 +696,7 @@ __device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, u
     float pna[3], pnb[3];
     read3c<ST>(pna, row, offan);
     read3c<ST>(pnb, row, offbn);
-#define NFN_FWD(A, B) flow_pair1<A, B>(z, l2, pa, pb)
+#define NFN_FWD(A, B) flow_pair1<A, B, ACCM>(z, l2, pa, pb)
     NFN_PAIR_SWITCH(ia * 3 + ib, NFN_FWD)
 #undef NFN_FWD
     ia = ian;
@@ -676,7 +708,7 @@ __device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, u
       pb[i] = pnb[i];
     }
   }
-  if (K & 1) l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(ia, z, pa)));  // the last flow: already read
+  if (K & 1) l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<ACCM>(ia, z, pa)));  // the last flow: already read
   return l2;
 }
 
@@ -684,7 +716,7 @@ __device__ __forceinline__ float chain1_fast_pairs(float& z, const float* row, u
 // covers a homogeneous chain): the pair's types and offsets are compile-time, the loop body
 // one basic block (no dispatch); U pairs per trip, the remainder pair by pair.  The same
 // flow_pair1 calls on the same values as chain1_fast_pairs.
-template <int IA, int IB, int U, int ST = 1>
+template <int IA, int IB, int U, int ST = 1, bool ACCM = true>
 __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, int K, int P) {
   constexpr int SA = IA == NFN_FLOW_AFFINE ? 2 : 3, SB = IB == NFN_FLOW_AFFINE ? 2 : 3, SP = SA + SB;
   float l2 = 0.0f;
@@ -701,14 +733,14 @@ __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, 
       float pna[3], pnb[3];
       read3c<ST>(pna, row, max(off - SA, 0));  // past flow 0: harmless in-row reads
       read3c<ST>(pnb, row, max(off - SP, 0));
-      flow_pair1<IA, IB>(z, l2, pa, pb);
+      flow_pair1<IA, IB, ACCM>(z, l2, pa, pb);
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         pa[i] = pna[i];
         pb[i] = pnb[i];
       }
     }
-    if (K & 1) l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));  // already read
+    if (K & 1) l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<ACCM>(IA, z, pa)));  // already read
     return l2;
   }
 #pragma unroll 1
@@ -720,7 +752,7 @@ __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, 
       read3c<ST>(pb[u], row, off - u * SP - SP);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) flow_pair1<IA, IB>(z, l2, pa[u], pb[u]);
+    for (int u = 0; u < U; ++u) flow_pair1<IA, IB, ACCM>(z, l2, pa[u], pb[u]);
     off -= U * SP;
   }
 #pragma unroll 1
@@ -728,13 +760,13 @@ __device__ __forceinline__ float chain1_fast_hpairs(float& z, const float* row, 
     float pa[3], pb[3];
     read3c<ST>(pa, row, off - SA);
     read3c<ST>(pb, row, off - SP);
-    flow_pair1<IA, IB>(z, l2, pa, pb);
+    flow_pair1<IA, IB, ACCM>(z, l2, pa, pb);
     off -= SP;
   }
   if (K & 1) {
     float pa[3];
     read3c<ST>(pa, row, off - SA);
-    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<ACCM>(IA, z, pa)));
   }
   return l2;
 }
@@ -811,19 +843,19 @@ __device__ __forceinline__ float base1_fast(float z, const float* row, bool trai
   return -0.5f * (z * z) - kHalfLog2Pi;
 }
 
-template <bool PACKED, int ST = 1, int CM = kChainLoop>
+template <bool PACKED, int ST = 1, int CM = kChainLoop, bool ACCM = true>
 __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, const ChainArgs& a) {
   const int K = a.prog.K;
   float l2 = 0.0f;  // sum of log2|det J_k|
   if constexpr (CM >= kChainHPair) {
     constexpr int c = CM - kChainHPair;
-    l2 = chain1_fast_hpairs<(c % 9) / 3, c % 3, c / 9, ST>(z, row, K, a.P);
+    l2 = chain1_fast_hpairs<(c % 9) / 3, c % 3, c / 9, ST, ACCM>(z, row, K, a.P);
   } else if constexpr (CM == kChainPairs) {
-    if (K > 0) l2 = chain1_fast_pairs<ST>(z, row, a.prog.types[0], K, a.P);
+    if (K > 0) l2 = chain1_fast_pairs<ST, ACCM>(z, row, a.prog.types[0], K, a.P);
   } else if constexpr (CM == kStaticProg) {
-    l2 = chain1_fast_static<kStaticTypes[0], kStaticK[0], ST>(z, row, a.P);
+    l2 = chain1_fast_static<kStaticTypes[0], kStaticK[0], ST, ACCM>(z, row, a.P);
   } else if constexpr (PACKED) {
-    if (K > 0) l2 = chain1_fast_packed<ST>(z, row, a.prog.types[0], K, a.P);
+    if (K > 0) l2 = chain1_fast_packed<ST, ACCM>(z, row, a.prog.types[0], K, a.P);
   } else if (K > 0) {
     int st = a.prog.step[0];
     float pc[3];
@@ -835,7 +867,7 @@ __device__ __forceinline__ float eval_chain1_fast(float z, const float* row, con
       const int id = st & 3;
       float l;
       if (id == NFN_FLOW_PLANAR)
-        l = planar1_fast(z, pc[0], pc[1], pc[2]);
+        l = planar1_fast<ACCM>(z, pc[0], pc[1], pc[2]);
       else if (id == NFN_FLOW_RADIAL)
         l = radial1_fast(z, pc[0], pc[1], pc[2]);
       else

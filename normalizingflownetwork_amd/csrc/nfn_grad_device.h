@@ -206,7 +206,7 @@ __device__ __forceinline__ void sp_sig1(float x, float& sp, float& sg) {
 }
 
 // z-only forward steps (the backward needs each flow's input, not its log-det).
-// (planar1_fast's z update, bitwise)
+// (planar1_fast<false>'s z update, bitwise: the backward keeps round 5's m, see planar1_fast)
 __device__ __forceinline__ void planar1_z(float& z, float u, float wraw, float b) {
   const float w = wraw + 1.0f;
   const float wtu = w * u;
@@ -333,7 +333,7 @@ __device__ __forceinline__ float grad1_packed(float& z, float* row, float* zh, i
       read3c<ST>(pn, row, offn);
       zh[k * zs] = z;
       if (want_lp) {
-        l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+        l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(id, z, pc)));
       } else if (id == NFN_FLOW_PLANAR) {
         planar1_z(z, pc[0], pc[1], pc[2]);
       } else if (id == NFN_FLOW_RADIAL) {
@@ -441,8 +441,8 @@ __device__ __forceinline__ void grad1_packed2(float& za, float& zb, float* ra, f
       zhb[k * zs] = zb;
       if (id == NFN_FLOW_PLANAR) {
         if (want_lp) {
-          l2a += __builtin_amdgcn_logf(fabsf(planar1_fast(za, pa[0], pa[1], pa[2])));
-          l2b += __builtin_amdgcn_logf(fabsf(planar1_fast(zb, pb[0], pb[1], pb[2])));
+          l2a += __builtin_amdgcn_logf(fabsf(planar1_fast<false>(za, pa[0], pa[1], pa[2])));
+          l2b += __builtin_amdgcn_logf(fabsf(planar1_fast<false>(zb, pb[0], pb[1], pb[2])));
         } else {
           planar1_z(za, pa[0], pa[1], pa[2]);
           planar1_z(zb, pb[0], pb[1], pb[2]);
@@ -540,12 +540,12 @@ __device__ __forceinline__ void fwd_pair1(float& z, float& l2, float& za, float&
                                           const float (&pb)[3], bool want_lp) {
   za = z;
   if (want_lp)
-    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(IA, z, pa)));
   else
     flow1_z(IA, z, pa);
   zb = z;
   if (want_lp)
-    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IB, z, pb)));
+    l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(IB, z, pb)));
   else
     flow1_z(IB, z, pb);
 }
@@ -595,7 +595,7 @@ __device__ __forceinline__ float grad1_pairs(float& z, float* row, float* zh, in
   if (K & 1) {  // the last flow: already read
     zh[(K - 1) * zs] = z;
     if (want_lp)
-      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(ia, z, pa)));
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(ia, z, pa)));
     else
       flow1_z(ia, z, pa);
   }
@@ -719,7 +719,7 @@ __device__ __forceinline__ float grad1_hpairs_regs(float& z, float* row, int K, 
     read3c<ST>(pa, row, P - np * SP - SA);
     zl = z;
     if (want_lp)
-      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(IA, z, pa)));
     else
       flow1_z(IA, z, pa);
   }
@@ -789,7 +789,7 @@ __device__ __forceinline__ float grad1_hpairs(float& z, float* row, float* zh, i
   if (K & 1) {  // the last flow: already read
     zh[(K - 1) * zs] = z;
     if (want_lp)
-      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(IA, z, pa)));
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(IA, z, pa)));
     else
       flow1_z(IA, z, pa);
   }
@@ -833,7 +833,7 @@ __device__ __forceinline__ float grad1_static(float& z, float* row, float* zh, i
     read3c<ST>(pc, row, off);
     zk[k] = z;
     if (want_lp)
-      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast(id, z, pc)));
+      l2 += __builtin_amdgcn_logf(fabsf(flow1_fast<false>(id, z, pc)));
     else
       flow1_z(id, z, pc);
   }

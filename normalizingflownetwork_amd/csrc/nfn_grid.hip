@@ -45,7 +45,7 @@ __device__ __forceinline__ void grid1_prepare(GridRow1& r, const float* row, con
         const float nw2 = fmaf(w, w, 1e-9f);
         const float rn = __builtin_amdgcn_rcpf(nw2);
         const float sp = softplus_alpha<true>(wtu);
-        const float m = sp - (1.0f - 1e-5f);
+        const float m = planar1_m(w, p[0], sp);
         r.c0[k] = w;
         r.c1[k] = p[2];
         r.c2[k] = planar1_uh(p[0], w, rn, m);

@@ -453,6 +453,11 @@ def make_planar_mdelta_r(R, deg, tanh=tanh_t3):
 
 for _R, _deg in ((0.75, 7), (1.5, 11), (2.0, 13), (3.0, 17)):
     FORMS[f"md{_R}"] = (make_planar_mdelta_r(_R, _deg), radial_r3, base_r3)
+# round 6's shipped form (csrc/nfn_device.h planar1_m): |d| <= 0.75, degree 7
+FORMS["r6"] = FORMS["md0.75"]
+# attribution: the round-6 m with an exact tanh / a wider polynomial range with an exact tanh
+FORMS["r6+tx"] = (make_planar_mdelta_r(0.75, 7, tanh=tanh_exact), radial_r3, base_r3)
+FORMS["md2.0+tx"] = (make_planar_mdelta_r(2.0, 13, tanh=tanh_exact), radial_r3, base_r3)
 
 
 if __name__ == "__main__":
