@@ -565,8 +565,13 @@ __host__ __device__ inline int dense1_grad_sb_wave_floats(int P, int K) {
 constexpr int kSbWRow = 16;  // dwords per hidden unit of the W parts (16 pairs of p, chunks swizzled as the planes)
 constexpr int kSbWFloats = 3 * 16 * kSbWRow + 32;  // the workgroup's W bf16 parts [part][hidden][pairs of p] and bias
 
+// CM: the chain form.  The diagnostic compile-time C2 program (kStaticProg, grad1_static) and
+// its parameter-scalar cache (kStaticCache, grad1_static_cache: 224 VGPRs) run at 2 waves per
+// SIMD (the static form spills at 3), every release form at 3.
+constexpr int kStaticCache = 4;
 template <int NN, int CM = kChainPairs>
-__global__ void __launch_bounds__(kMaxBlock, 3) chain_dense1_grad_sb_kernel(DenseGradArgs g) {
+__global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStaticProg) ? 2 : 3)
+    chain_dense1_grad_sb_kernel(DenseGradArgs g) {
   static_assert(NN == 1 || NN == 2, "P <= 32");
   const DenseArgs& da = g.da;
   const ChainArgs& a = da.c;
@@ -704,7 +709,13 @@ __global__ void __launch_bounds__(kMaxBlock, 3) chain_dense1_grad_sb_kernel(Dens
     // 3. the chain forward + reverse per lane: the t column entries become g * d logp / d t
     float adj, z = z0;
     float lp;
-    if constexpr (CM >= kChainHPair)
+    if constexpr (CM == kStaticCache)
+      lp = grad1_static_cache<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, P, trainable, gl, a.out != nullptr,
+                                                                  adj) - corr;
+    else if constexpr (CM == kStaticProg)
+      lp = grad1_static<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, zh, 64, P, trainable, gl, a.out != nullptr,
+                                                            adj) - corr;
+    else if constexpr (CM >= kChainHPair)
       lp = grad1_hpairs<((CM - kChainHPair) % 9) / 3, (CM - kChainHPair) % 3, kCS>(
                z, tl + lane, zh, 64, K, P, trainable, gl, a.out != nullptr, adj) - corr;
     else if constexpr (CM == kChainPairs)
@@ -888,8 +899,20 @@ constexpr int kDgradSplitBf16 = 1;
 template <int NN>
 int64_t launch_dg1_sb(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
   auto kfn = chain_dense1_grad_sb_kernel<NN, kChainPairs>;
+  // C2's program, (planar, radial) x 5, at compile time with the parameter-scalar cache: 0.977 vs
+  // 1.066 ms without the cache and 1.158 for the runtime program's pair form in one bench-harness
+  // A/B (profiles/r06/r06i_*); the diag build's NFN_CHAIN_FORM picks the others
+  const bool c2prog = NN == 2 && g.da.c.prog.K == kStaticK[0] && g.da.c.prog.types[0] == kStaticTypes[0];
+  if constexpr (NN == 2) {
+    if (c2prog) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCache>;
+  }
 #ifdef NFN_DIAG
-  if (env_int("NFN_CHAIN_FORM", kChainPairs) == kChainLoop) kfn = chain_dense1_grad_sb_kernel<NN, kChainLoop>;
+  const int cf = env_int("NFN_CHAIN_FORM", -1);
+  if (cf == kChainLoop) kfn = chain_dense1_grad_sb_kernel<NN, kChainLoop>;
+  if (cf == kChainPairs) kfn = chain_dense1_grad_sb_kernel<NN, kChainPairs>;
+  if constexpr (NN == 2) {
+    if (c2prog && cf == kStaticProg) kfn = chain_dense1_grad_sb_kernel<NN, kStaticProg>;
+  }
 #endif
   const size_t lds = ((size_t)4 * dense1_grad_sb_wave_floats(g.da.c.P, g.da.c.prog.K) + kSbWFloats) * sizeof(float);
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (g.da.c.ntiles + 3) / 4);

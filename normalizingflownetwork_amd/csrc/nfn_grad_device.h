@@ -864,6 +864,146 @@ __device__ __forceinline__ float grad1_static(float& z, float* row, float* zh, i
   return lp;
 }
 
+// grad1_static with a parameter-scalar cache (verdict r05 "Next" 2) — the fused Dense
+// backward's form for a program fixed at compile time (C2's (planar, radial) x 5): the forward
+// pass forms, per flow, every parameter-only scalar the reverse pass needs (planar: sigma(w u),
+// 1 / |w|^2, c / |w|^2, u_hat, m and the det's parameter term; radial: alpha,
+// sigma(0.3 a - 2), sigma(0.1 b + log(e - 1)), alpha beta, beta) once, from one exponential per
+// softplus, and keeps them in registers (the program is a compile-time constant, so the cache is
+// plain unrolled locals: 224 VGPRs, 2 waves per SIMD) instead of the reverse pass recomputing
+// them (per planar flow an exp, two rcp and a log; per radial two of each).  Values: bitwise
+// grad1_static's (the same expressions on the same operands; tests/test_gpu_diag.py).
+template <uint32_t TYPES, int K, int ST = 1>
+__device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P, bool trainable, float gl,
+                                                    bool want_lp, float& adj) {
+  float l2 = 0.0f;
+  float zk[K], c0[K], c1[K], c2[K], c3[K], c4[K], c5[K];
+  int off = P;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int id = (int)((TYPES >> (2 * k)) & 3u);
+    off -= size1(id);
+    float pc[3];
+    read3c<ST>(pc, row, off);
+    zk[k] = z;
+    if (id == NFN_FLOW_PLANAR) {
+      const float u = pc[0], w = pc[1] + 1.0f, b = pc[2];
+      const float wtu = w * u;
+      float sp, sg;
+      sp_sig1<true>(wtu, sp, sg);  // sp: softplus_alpha's value bitwise
+      const float nw2 = fmaf(w, w, 1e-9f);
+      const float rn = __builtin_amdgcn_rcpf(nw2);
+      // the forward: planar1_z / planar1_fast<false> bitwise
+      const float mf = sp - (1.0f - 1e-5f);
+      const float uhf = planar1_uh(u, w, rn, mf);
+      const float th = tanh_fast(fmaf(w, z, b));
+      z = fmaf(uhf, th, z);
+      if (want_lp) {
+        const float qd = fmaf((wtu - mf) * 1e-9f, rn, sp + 1e-5f);
+        l2 += __builtin_amdgcn_logf(fabsf(fmaf(th, th, fmaf(-th, th, 1.0f) * qd)));
+      }
+      // the reverse pass's parameter scalars (planar1_bwd's expressions)
+      const float m = (sp - 1.0f) + 1e-5f;
+      const float c = m - wtu;
+      const float q0 = c * rn;
+      const float cn = fmaf(fmaf(-nw2, q0, c), rn, q0);
+      c0[k] = sg;
+      c1[k] = rn;
+      c2[k] = cn;
+      c3[k] = planar1_uh(u, w, rn, m);
+      c4[k] = m;
+      c5[k] = fmaf(-cn, 1e-9f, sp + 1e-5f);
+    } else if (id == NFN_FLOW_RADIAL) {
+      const float xa = fmaf(0.3f, pc[0], -2.0f);
+      const float xb = fmaf(0.1f, pc[1], kLogExpm1One);
+      float al, sga, spb, sgb;
+      sp_sig1<true>(xa, al, sga);  // al: softplus_alpha's value bitwise
+      sp_sig1(xb, spb, sgb);       // spb: sp_fast1's value bitwise
+      const float ab = fmaf(al, spb, -al);
+      const float dz = z - pc[2];
+      const float h = __builtin_amdgcn_rcpf(al + fabsf(dz));
+      const float abh = ab * h;
+      z = fmaf(abh, dz, z);  // radial1_z / radial1_fast bitwise
+      if (want_lp) l2 += __builtin_amdgcn_logf(fabsf(fmaf(abh, al * h, 1.0f)));
+      c0[k] = al;
+      c1[k] = sga;
+      c2[k] = sgb;
+      c3[k] = ab;
+      c4[k] = spb - 1.0f;
+      c5[k] = 0.0f;
+    } else {
+      const float sc = 1.0f + pc[1];
+      if (want_lp) l2 += __builtin_amdgcn_logf(fabsf(sc));
+      z = fmaf(z, sc, pc[0]);
+      c0[k] = c1[k] = c2[k] = c3[k] = c4[k] = c5[k] = 0.0f;
+    }
+  }
+  const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
+  float a;
+  if (trainable) {
+    float sps, sgs;
+    sp_sig1(kLogExpm1One + 0.1f * row[ST], sps, sgs);
+    const float rs = __builtin_amdgcn_rcpf(1e-3f + sps);
+    const float zz = (z - row[0]) * rs;
+    const float gz = gl * zz * rs;
+    a = -gz;
+    row[0] = gz;
+    row[ST] = 0.1f * sgs * gl * fmaf(zz, zz, -1.0f) * rs;
+  } else {
+    a = -gl * z;
+  }
+  int ob = trainable ? 2 : 0;
+#pragma unroll
+  for (int k = K - 1; k >= 0; --k) {
+    const int id = (int)((TYPES >> (2 * k)) & 3u);
+    float pc[3];
+    read3c<ST>(pc, row, ob);
+    float* p = row + ob * ST;
+    const float zz = zk[k];
+    if (id == NFN_FLOW_PLANAR) {  // planar1_bwd with the cached scalars
+      const float u = pc[0], w = pc[1] + 1.0f;
+      const float sg = c0[k], rn = c1[k], cn = c2[k], uh = c3[k], m = c4[k], qd0 = c5[k];
+      const float s = fmaf(w, zz, pc[2]);
+      const float E = __builtin_amdgcn_exp2f(fabsf(s) * (-2.0f * kLog2e));
+      const float rE = __builtin_amdgcn_rcpf(1.0f + E);
+      const float h = copysignf((1.0f - E) * rE, s);
+      const float hp = 4.0f * E * rE * rE;
+      const float q = fmaf(-cn, 1e-9f, m);
+      const float hpd = gl * hp * __builtin_amdgcn_rcpf(fmaf(h, h, hp * qd0));
+      const float Ss = fmaf(hp, uh * a, -2.0f * q * h * hpd);
+      const float G = fmaf(h, a, hpd * w);
+      const float wGn = w * G * rn;
+      const float k1 = (sg - 1.0f) * wGn;
+      p[0] = G * (fmaf(sg * w, w, 1e-9f) * rn);
+      p[ST] = fmaf(zz, Ss, fmaf(hpd, uh, fmaf(cn, G, fmaf(-2.0f * cn * wGn, w, k1 * u))));
+      p[2 * ST] = Ss;
+      a = fmaf(w, Ss, a);
+    } else if (id == NFN_FLOW_RADIAL) {  // radial1_bwd with the cached scalars
+      const float al = c0[k], sga = c1[k], sgb = c2[k], ab = c3[k], be = c4[k];
+      const float dz = zz - pc[2];
+      const float h = __builtin_amdgcn_rcpf(al + fabsf(dz));
+      const float hh = h * h;
+      const float rB = __builtin_amdgcn_rcpf(fmaf(ab * al, hh, 1.0f));
+      const float da = dz * a;
+      const float glr = gl * rB;
+      const float H = fmaf(ab, da, 2.0f * ab * al * h * glr);
+      const float g_ab = fmaf(h, da, al * hh * glr);
+      const float g_al = fmaf(be, g_ab, ab * hh * glr) - hh * H;
+      const float hH = hh * H;
+      const float sgn = sign0(dz);
+      p[0] = 0.3f * sga * g_al;
+      p[ST] = 0.1f * sgb * al * g_ab;
+      p[2 * ST] = fmaf(hH, sgn, -ab * h * a);
+      a = fmaf(fmaf(ab, h, 1.0f), a, -hH * sgn);
+    } else {
+      affine1_bwd<ST>(zz, a, pc[0], pc[1], p, gl);
+    }
+    ob += size1(id);
+  }
+  adj = a;
+  return lp;
+}
+
 // ---------------------------------------------------------------------------
 // Lane-group forms (d >= 4): a G-lane group owns one sample, lane j holds the
 // DPL dimensions j, j + G, ...; inner products are DPP group sums (gsum).

@@ -203,6 +203,46 @@ def flow_tile():
     return res
 
 
+def dense_cache():
+    """The fused Dense backward's parameter-scalar cache (the release form for C2's program,
+    grad1_static_cache; NFN_CHAIN_FORM=4 names it) against the same compile-time program without
+    it (diag NFN_CHAIN_FORM=2, grad1_static): the reverse pass takes the scalars the forward
+    formed with the same expressions, so log_prob, dh, dW, db and dy must be bitwise equal; and
+    both within 1e-5 of the runtime program's pair form (diag NFN_CHAIN_FORM=3) on the
+    well-conditioned entries."""
+    import torch
+
+    from normalizingflownetwork_amd import _lib
+
+    _lib.use_diagnostic_build()
+    from normalizingflownetwork_amd import ops
+
+    res = {"library": os.path.basename(_lib.LIB_PATH)}
+    ft = ("planar", "radial") * 5
+    for B in (64 * 37 + 5, 1 << 16):
+        gen = torch.Generator(device="cuda").manual_seed(B)
+        y = torch.randn((B, 1), generator=gen, device="cuda")
+        h = torch.randn((B, 16), generator=gen, device="cuda")
+        W = torch.randn((16, 32), generator=gen, device="cuda") / 4.0
+        b = 0.1 * torch.randn((32,), generator=gen, device="cuda")
+        g = torch.randn((B,), generator=gen, device="cuda")
+        outs = {}
+        for cm in ("3", "2", "4"):
+            os.environ["NFN_CHAIN_FORM"] = cm
+            try:
+                outs[cm] = ops.chain_log_prob_dense_grad(y, h, W, b, ft, 1, True, g_out=g, want_logp=True)
+            finally:
+                os.environ.pop("NFN_CHAIN_FORM")
+        for x2, x4, what in zip(outs["2"], outs["4"], ("log_prob", "dh", "dW", "db", "dy")):
+            same = (x2 == x4) | (torch.isnan(x2) & torch.isnan(x4))
+            assert bool(same.all()), f"B={B} {what}: {int((~same).sum())} values differ (cache vs static)"
+        lp3, lp2 = outs["3"][0], outs["2"][0]
+        ok = torch.isfinite(lp3) & (lp3.abs() < 1e4)
+        assert torch.allclose(lp2[ok], lp3[ok], rtol=1e-5, atol=1e-5), f"B={B}: static vs pairs log_prob"
+        res[f"B{B}"] = "bitwise"
+    return res
+
+
 def tanh():
     """tanh_fast (the planar flows' tanh in every fast-math kernel) on the device against fp64
     over a dense sweep of [-1, 1] (where the two branches meet, at |a| = 0.3) and a coarser one
@@ -260,4 +300,4 @@ def release():
 if __name__ == "__main__":
     which = sys.argv[1]
     print(json.dumps({which: {"strategies": strategies, "release": release, "grad_stream": grad_stream, "flow_tile": flow_tile,
-                             "densep": densep, "tanh": tanh}[which]()}), flush=True)
+                             "densep": densep, "tanh": tanh, "dense_cache": dense_cache}[which]()}), flush=True)

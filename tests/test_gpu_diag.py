@@ -76,3 +76,11 @@ def test_diag_tanh_fast_ulp_bound(gpu):
     assert res["library"] == "libnfn_hip_diag.so"
     assert res["sweep_1"]["max_ulp"] <= 3.25, res["sweep_1"]
     assert res["sweep_12"]["max_ulp"] <= 3.25, res["sweep_12"]
+
+
+def test_diag_dense_grad_scalar_cache_bitwise(gpu):
+    """The fused Dense backward's parameter-scalar cache (verdict r05; the release form for C2's
+    program) gives the uncached compile-time program's values bitwise."""
+    res = _run("dense_cache")
+    assert res["library"] == "libnfn_hip_diag.so"
+    assert sum(v == "bitwise" for v in res.values()) == 2
