@@ -565,12 +565,13 @@ __host__ __device__ inline int dense1_grad_sb_wave_floats(int P, int K) {
 constexpr int kSbWRow = 16;  // dwords per hidden unit of the W parts (16 pairs of p, chunks swizzled as the planes)
 constexpr int kSbWFloats = 3 * 16 * kSbWRow + 32;  // the workgroup's W bf16 parts [part][hidden][pairs of p] and bias
 
-// CM: the chain form.  The diagnostic compile-time C2 program (kStaticProg, grad1_static) and
-// its parameter-scalar cache (kStaticCache, grad1_static_cache: 224 VGPRs) run at 2 waves per
-// SIMD (the static form spills at 3), every release form at 3.
-constexpr int kStaticCache = 4;
+// CM: the chain form.  The compile-time C2 program (diag kStaticProg, grad1_static) and its
+// parameter-scalar cache (kStaticCache, grad1_static_cache: the release form for C2's program;
+// diag kStaticCacheX, the cache bitwise grad1_static's) run at 2 waves per SIMD (the static
+// form spills at 3), every other form at 3.
+constexpr int kStaticCache = 4, kStaticCacheX = 5;
 template <int NN, int CM = kChainPairs>
-__global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStaticProg) ? 2 : 3)
+__global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStaticCacheX || CM == kStaticProg) ? 2 : 3)
     chain_dense1_grad_sb_kernel(DenseGradArgs g) {
   static_assert(NN == 1 || NN == 2, "P <= 32");
   const DenseArgs& da = g.da;
@@ -709,9 +710,9 @@ __global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStati
     // 3. the chain forward + reverse per lane: the t column entries become g * d logp / d t
     float adj, z = z0;
     float lp;
-    if constexpr (CM == kStaticCache)
-      lp = grad1_static_cache<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, P, trainable, gl, a.out != nullptr,
-                                                                  adj) - corr;
+    if constexpr (CM == kStaticCache || CM == kStaticCacheX)
+      lp = grad1_static_cache<kStaticTypes[0], kStaticK[0], kCS, CM == kStaticCache>(z, tl + lane, P, trainable, gl,
+                                                                                      a.out != nullptr, adj) - corr;
     else if constexpr (CM == kStaticProg)
       lp = grad1_static<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, zh, 64, P, trainable, gl, a.out != nullptr,
                                                             adj) - corr;
@@ -912,6 +913,7 @@ int64_t launch_dg1_sb(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) 
   if (cf == kChainPairs) kfn = chain_dense1_grad_sb_kernel<NN, kChainPairs>;
   if constexpr (NN == 2) {
     if (c2prog && cf == kStaticProg) kfn = chain_dense1_grad_sb_kernel<NN, kStaticProg>;
+    if (c2prog && cf == kStaticCacheX) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCacheX>;
   }
 #endif
   const size_t lds = ((size_t)4 * dense1_grad_sb_wave_floats(g.da.c.P, g.da.c.prog.K) + kSbWFloats) * sizeof(float);

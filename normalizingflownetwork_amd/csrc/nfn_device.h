@@ -293,14 +293,17 @@ __device__ __forceinline__ float softplus_alpha(float x) {
 // bought nothing over this one in the fp32 emulation of the C2 chain (tools/kernel_emu.py: 200
 // vs 206 of 2^21 samples beyond 3e-6 relative, 5 vs 5 beyond 1e-5) and cost two VALU per planar
 // flow, which the C2 stream pays for (profiles/r05/).
+__device__ __forceinline__ float tanh_poly03(float a) {  // |a| < 0.3
+  const float a2 = a * a;
+  float p = fmaf(a2, -0.050372913f, 0.13314915f);
+  p = fmaf(a2, p, -0.33333063f);
+  return fmaf(a * a2, p, a);
+}
 __device__ __forceinline__ float tanh_fast(float a) {
   const float x = fabsf(a);
   const float E = __builtin_amdgcn_exp2f(x * (2.0f * kLog2e));
   const float te = copysignf(1.0f - __builtin_amdgcn_rcpf(fmaf(E, 0.5f, 0.5f)), a);
-  const float a2 = a * a;
-  float p = fmaf(a2, -0.050372913f, 0.13314915f);
-  p = fmaf(a2, p, -0.33333063f);
-  const float tp = fmaf(a * a2, p, a);
+  const float tp = tanh_poly03(a);
   return x < 0.3f ? tp : te;
 }
 

@@ -871,13 +871,19 @@ __device__ __forceinline__ float grad1_static(float& z, float* row, float* zh, i
 // sigma(0.3 a - 2), sigma(0.1 b + log(e - 1)), alpha beta, beta) once, from one exponential per
 // softplus, and keeps them in registers (the program is a compile-time constant, so the cache is
 // plain unrolled locals: 224 VGPRs, 2 waves per SIMD) instead of the reverse pass recomputing
-// them (per planar flow an exp, two rcp and a log; per radial two of each).  Values: bitwise
-// grad1_static's (the same expressions on the same operands; tests/test_gpu_diag.py).
-template <uint32_t TYPES, int K, int ST = 1>
+// them (per planar flow an exp, two rcp and a log; per radial two of each).  Each radial flow
+// also keeps h = 1 / (alpha + |z - z0|), the same rcp on the same operands in both passes.
+// SHARE (the release form) goes one step further for the planar flows: the forward evaluates
+// the reverse pass's e^{-2|s|} form of tanh(s) (s = w z + b) once and keeps tanh and tanh'
+// for the reverse, taking tanh(s) from it for |s| >= 0.3 (tanh_poly03 below, as tanh_fast)
+// instead of tanh_fast's e^{2|s|} form: one exp and one rcp fewer per planar flow, forward
+// values within a few ulp of tanh_fast's.  !SHARE (diag NFN_CHAIN_FORM=5): bitwise
+// grad1_static's values (the same expressions on the same operands; tests/test_gpu_diag.py).
+template <uint32_t TYPES, int K, int ST = 1, bool SHARE = true>
 __device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P, bool trainable, float gl,
                                                     bool want_lp, float& adj) {
   float l2 = 0.0f;
-  float zk[K], c0[K], c1[K], c2[K], c3[K], c4[K], c5[K];
+  float zk[K], c0[K], c1[K], c2[K], c3[K], c4[K], c5[K], c6[K], c7[K];
   int off = P;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -896,7 +902,19 @@ __device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P,
       // the forward: planar1_z / planar1_fast<false> bitwise
       const float mf = sp - (1.0f - 1e-5f);
       const float uhf = planar1_uh(u, w, rn, mf);
-      const float th = tanh_fast(fmaf(w, z, b));
+      const float sv = fmaf(w, z, b);
+      float th;
+      if constexpr (SHARE) {  // planar1_bwd's tanh and tanh' of s
+        const float E = __builtin_amdgcn_exp2f(fabsf(sv) * (-2.0f * kLog2e));
+        const float rE = __builtin_amdgcn_rcpf(1.0f + E);
+        const float hE = copysignf((1.0f - E) * rE, sv);
+        c6[k] = hE;
+        c7[k] = 4.0f * E * rE * rE;
+        th = fabsf(sv) < 0.3f ? tanh_poly03(sv) : hE;
+      } else {
+        th = tanh_fast(sv);
+        c6[k] = c7[k] = 0.0f;
+      }
       z = fmaf(uhf, th, z);
       if (want_lp) {
         const float qd = fmaf((wtu - mf) * 1e-9f, rn, sp + 1e-5f);
@@ -925,6 +943,8 @@ __device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P,
       const float abh = ab * h;
       z = fmaf(abh, dz, z);  // radial1_z / radial1_fast bitwise
       if (want_lp) l2 += __builtin_amdgcn_logf(fabsf(fmaf(abh, al * h, 1.0f)));
+      c6[k] = h;
+      c7[k] = 0.0f;
       c0[k] = al;
       c1[k] = sga;
       c2[k] = sgb;
@@ -935,7 +955,7 @@ __device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P,
       const float sc = 1.0f + pc[1];
       if (want_lp) l2 += __builtin_amdgcn_logf(fabsf(sc));
       z = fmaf(z, sc, pc[0]);
-      c0[k] = c1[k] = c2[k] = c3[k] = c4[k] = c5[k] = 0.0f;
+      c0[k] = c1[k] = c2[k] = c3[k] = c4[k] = c5[k] = c6[k] = c7[k] = 0.0f;
     }
   }
   const float lp = want_lp ? base1_fast<ST>(z, row, trainable) + l2 * kLn2 : 0.0f;
@@ -963,11 +983,17 @@ __device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P,
     if (id == NFN_FLOW_PLANAR) {  // planar1_bwd with the cached scalars
       const float u = pc[0], w = pc[1] + 1.0f;
       const float sg = c0[k], rn = c1[k], cn = c2[k], uh = c3[k], m = c4[k], qd0 = c5[k];
-      const float s = fmaf(w, zz, pc[2]);
-      const float E = __builtin_amdgcn_exp2f(fabsf(s) * (-2.0f * kLog2e));
-      const float rE = __builtin_amdgcn_rcpf(1.0f + E);
-      const float h = copysignf((1.0f - E) * rE, s);
-      const float hp = 4.0f * E * rE * rE;
+      float h, hp;
+      if constexpr (SHARE) {
+        h = c6[k];
+        hp = c7[k];
+      } else {
+        const float s = fmaf(w, zz, pc[2]);
+        const float E = __builtin_amdgcn_exp2f(fabsf(s) * (-2.0f * kLog2e));
+        const float rE = __builtin_amdgcn_rcpf(1.0f + E);
+        h = copysignf((1.0f - E) * rE, s);
+        hp = 4.0f * E * rE * rE;
+      }
       const float q = fmaf(-cn, 1e-9f, m);
       const float hpd = gl * hp * __builtin_amdgcn_rcpf(fmaf(h, h, hp * qd0));
       const float Ss = fmaf(hp, uh * a, -2.0f * q * h * hpd);
@@ -981,7 +1007,7 @@ __device__ __forceinline__ float grad1_static_cache(float& z, float* row, int P,
     } else if (id == NFN_FLOW_RADIAL) {  // radial1_bwd with the cached scalars
       const float al = c0[k], sga = c1[k], sgb = c2[k], ab = c3[k], be = c4[k];
       const float dz = zz - pc[2];
-      const float h = __builtin_amdgcn_rcpf(al + fabsf(dz));
+      const float h = c6[k];
       const float hh = h * h;
       const float rB = __builtin_amdgcn_rcpf(fmaf(ab * al, hh, 1.0f));
       const float da = dz * a;

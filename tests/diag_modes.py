@@ -204,12 +204,14 @@ def flow_tile():
 
 
 def dense_cache():
-    """The fused Dense backward's parameter-scalar cache (the release form for C2's program,
-    grad1_static_cache; NFN_CHAIN_FORM=4 names it) against the same compile-time program without
-    it (diag NFN_CHAIN_FORM=2, grad1_static): the reverse pass takes the scalars the forward
-    formed with the same expressions, so log_prob, dh, dW, db and dy must be bitwise equal; and
-    both within 1e-5 of the runtime program's pair form (diag NFN_CHAIN_FORM=3) on the
-    well-conditioned entries."""
+    """The fused Dense backward's parameter-scalar cache for C2's compile-time program.  The
+    exact cache (diag NFN_CHAIN_FORM=5: the reverse pass takes the scalars the forward formed
+    with the same expressions) against the uncached program (diag NFN_CHAIN_FORM=2,
+    grad1_static): log_prob, dh, dW, db and dy bitwise equal.  The release form (=4, which also
+    shares planar tanh / tanh' between the passes, tanh(s) from the e^{-2|s|} form for
+    |s| >= 0.3): log_prob within 1e-5 of the uncached program's on the well-conditioned entries,
+    and the gradients' relative differences recorded (test_gpu_dense gates them on the oracle);
+    the pair form of the runtime program (=3) within 1e-5 likewise."""
     import torch
 
     from normalizingflownetwork_amd import _lib
@@ -219,6 +221,7 @@ def dense_cache():
 
     res = {"library": os.path.basename(_lib.LIB_PATH)}
     ft = ("planar", "radial") * 5
+    names = ("log_prob", "dh", "dW", "db", "dy")
     for B in (64 * 37 + 5, 1 << 16):
         gen = torch.Generator(device="cuda").manual_seed(B)
         y = torch.randn((B, 1), generator=gen, device="cuda")
@@ -227,19 +230,26 @@ def dense_cache():
         b = 0.1 * torch.randn((32,), generator=gen, device="cuda")
         g = torch.randn((B,), generator=gen, device="cuda")
         outs = {}
-        for cm in ("3", "2", "4"):
+        for cm in ("3", "2", "4", "5"):
             os.environ["NFN_CHAIN_FORM"] = cm
             try:
                 outs[cm] = ops.chain_log_prob_dense_grad(y, h, W, b, ft, 1, True, g_out=g, want_logp=True)
             finally:
                 os.environ.pop("NFN_CHAIN_FORM")
-        for x2, x4, what in zip(outs["2"], outs["4"], ("log_prob", "dh", "dW", "db", "dy")):
-            same = (x2 == x4) | (torch.isnan(x2) & torch.isnan(x4))
-            assert bool(same.all()), f"B={B} {what}: {int((~same).sum())} values differ (cache vs static)"
-        lp3, lp2 = outs["3"][0], outs["2"][0]
-        ok = torch.isfinite(lp3) & (lp3.abs() < 1e4)
-        assert torch.allclose(lp2[ok], lp3[ok], rtol=1e-5, atol=1e-5), f"B={B}: static vs pairs log_prob"
-        res[f"B{B}"] = "bitwise"
+        for x2, x5, what in zip(outs["2"], outs["5"], names):
+            same = (x2 == x5) | (torch.isnan(x2) & torch.isnan(x5))
+            assert bool(same.all()), f"B={B} {what}: {int((~same).sum())} values differ (exact cache vs static)"
+        lp2 = outs["2"][0]
+        ok = torch.isfinite(lp2) & (lp2.abs() < 1e4)
+        for cm in ("3", "4"):
+            assert torch.allclose(outs[cm][0][ok], lp2[ok], rtol=1e-5, atol=1e-5), f"B={B}: form {cm} vs static log_prob"
+        rel = {}
+        for x2, x4, what in zip(outs["2"], outs["4"], names):
+            fin = torch.isfinite(x2) & torch.isfinite(x4)
+            r = ((x4 - x2).abs() / x2.abs().clamp_min(1.0))[fin].double()
+            rel[what] = {"max": float(r.max()), "p999": float(torch.quantile(r[:1 << 20], 0.999)),
+                         "n_beyond_1e-5": int((r > 1e-5).sum()), "n": int(r.numel())}
+        res[f"B{B}"] = {"exact_cache": "bitwise", "shared_vs_static": rel}
     return res
 
 

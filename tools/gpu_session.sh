@@ -86,6 +86,7 @@ for s in $STEPS; do
     c3micro) run c3micro 300 python tools/microbench.py c3 ;;
     dense) run bench_dense 300 python bench.py --mode dense --steps 50 --warmup 10 --cpu-seconds 6 ;;
     densetests) run densetests 300 python -u -m pytest tests/test_gpu_dense.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    diagtests) run diagtests 300 python -u -m pytest tests/test_gpu_diag.py -m gpu -v -s -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     gradtests) run gradtests 300 python -u -m pytest tests/test_gpu_grad.py -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     grad_c3_nocpu) run bench_grad_c3 300 python bench.py --mode grad --config C3 --steps 20 --warmup 5 --no-cpu-baseline ;;
     dgradmicro) run dgradmicro 300 python tools/microbench.py dgrad ;;
