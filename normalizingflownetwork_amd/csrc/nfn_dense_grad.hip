@@ -569,7 +569,6 @@ constexpr int kSbWFloats = 3 * 16 * kSbWRow + 32;  // the workgroup's W bf16 par
 // parameter-scalar cache (kStaticCache, grad1_static_cache: the release form for C2's program;
 // diag kStaticCacheX, the cache bitwise grad1_static's) run at 2 waves per SIMD (the static
 // form spills at 3), every other form at 3.
-constexpr int kStaticCache = 4, kStaticCacheX = 5;
 template <int NN, int CM = kChainPairs>
 __global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStaticCacheX || CM == kStaticProg) ? 2 : 3)
     chain_dense1_grad_sb_kernel(DenseGradArgs g) {

@@ -821,8 +821,10 @@ __device__ __forceinline__ void chain1_fast_pairs2(float& za, float& zb, const f
 }
 
 // Chain-evaluation form of the d = 1 kernels: the packed loop, two flows per dispatch,
-// or (diagnostic experiment) one compile-time program, C2's.
-constexpr int kChainLoop = 0, kStaticProg = 2, kChainPairs = 3;
+// or one compile-time program, C2's: without (diagnostic) / with the backward's
+// parameter-scalar cache (grad1_static_cache: kStaticCache shares planar tanh between
+// the passes, kStaticCacheX is bitwise grad1_static).
+constexpr int kChainLoop = 0, kStaticProg = 2, kChainPairs = 3, kStaticCache = 4, kStaticCacheX = 5;
 // Alternating-type programs (chain1_fast_hpairs): CM = hpair_form(IA, IB, U), U pairs per
 // loop trip.
 constexpr int kChainHPair = 8;
