@@ -12,6 +12,7 @@
 //      B = W from the workgroup's LDS copy, four 16-row M tiles per 16-column N tile;
 //      accumulators + bias are written into the wave's t tile (odd stride);
 //   3. the chain runs per lane exactly as in chain_persistent_kernel.
+#include "nfn_bf16.h"
 #include "nfn_launch.h"
 
 namespace nfn {
@@ -147,8 +148,23 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense_kernel(DenseArgs da) {
 // after the next prefetch, no branch between a load and its use.  QH = H / 4.
 // NN = 16-column N tiles of t (P <= 16 NN), a compile-time count so the GEMM unrolls
 // and the tile's A fragments are read from LDS once for all N tiles.
-template <int QH, int NN, int CM = kChainLoop>
+// SB (H = 16, P <= 32): t = h W on v_mfma_f32_16x16x32_bf16 with exact 3-way splits
+// (nfn_bf16.h) instead of v_mfma_f32_16x16x4_f32.  K = 32 holds two parts of the 16 hidden
+// units, so the six products take three MFMAs per 16 x 16 block of t:
+//   [h3 | h2] x [W1 ; W2],  [h1 | h1] x [W3 ; W2],  [h2 | h1] x [W1 ; W1]  (smallest first),
+// lane group g = lane >> 4 holding K slots 8 g .. 8 g + 7 = hidden 8 (g & 1) + j of part
+// (g < 2 ? first : second).  W is split once per launch into registers; h is split once per
+// tile at the hand-off, each loading lane writing its float4's three parts (ds_write_b64)
+// into three bf16 planes [row][16] of the wave's slot, read back as one ds_read_b128 per
+// fragment (rows 16 mt + lane % 16, chunk g & 1: conflict-free in the guide's b128 lane
+// groups).
+constexpr int kSbPlane = 64 * 8;  // dwords per bf16 plane of the h tile (64 rows x 16 bf16)
+__host__ __device__ inline int dense1_sb_wave_floats(int P, int SH) {
+  return std::max(dense1_wave_floats(P, SH), 3 * kSbPlane);
+}
+template <int QH, int NN, int CM = kChainLoop, bool SB = false>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
+  static_assert(!SB || (QH == 4 && NN <= 2), "split-bf16 t: H = 16, P <= 32");
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
   __shared__ double red[2 * kMaxBlock / 64];
@@ -167,7 +183,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   // chain's read-ahead, overlaying the h tile: a wave's t writes follow its own A
   // fragment reads of h in LDS program order
   float* wl = lds;
-  float* hl = lds + H * NP + wid * dense1_wave_floats(P, SH);
+  float* hl = lds + H * NP + wid * (SB ? dense1_sb_wave_floats(P, SH) : dense1_wave_floats(P, SH));
   float* tl = hl;
   for (int i = tid; i < H * NP; i += blockDim.x) {
     const int k = i / NP, n = i - (i / NP) * NP;
@@ -181,11 +197,29 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   // B fragments (W) stay in registers for the whole launch when they are few
   constexpr bool kBReg = QH * NN <= 16;
   float bvr[kBReg ? QH : 1][kBReg ? NN : 1];
-  if constexpr (kBReg) {
+  if constexpr (kBReg && !SB) {
 #pragma unroll
     for (int ks = 0; ks < QH; ++ks)
 #pragma unroll
       for (int nt = 0; nt < NN; ++nt) bvr[ks][nt] = wl[(4 * ks + ak) * NP + 16 * nt + am];
+  }
+  // SB: the B fragments of the three MFMAs per N tile, [W1 ; W2], [W3 ; W2], [W1 ; W1]
+  // (lane: column 16 nt + am, hidden 8 (ak & 1) + j, part by ak < 2)
+  bf16x8v wsb[SB ? NN : 1][3];
+  if constexpr (SB) {
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) {
+      uint32_t w1[4], w2[4], w3[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k0 = 8 * (ak & 1) + 2 * q;
+        split3_pk(wl[k0 * NP + 16 * nt + am], wl[(k0 + 1) * NP + 16 * nt + am], w1[q], w2[q], w3[q]);
+      }
+      const bool lo = ak < 2;
+      wsb[nt][0] = lo ? frag8(w1[0], w1[1], w1[2], w1[3]) : frag8(w2[0], w2[1], w2[2], w2[3]);
+      wsb[nt][1] = lo ? frag8(w3[0], w3[1], w3[2], w3[3]) : frag8(w2[0], w2[1], w2[2], w2[3]);
+      wsb[nt][2] = frag8(w1[0], w1[1], w1[2], w1[3]);
+    }
   }
   const int64_t hs = da.h_rowstride;
   const int64_t ntiles = a.ntiles;
@@ -227,18 +261,60 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   for (int64_t tile = u0; tile < ntiles; tile += ustep) {
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
+    if constexpr (SB) {  // the three bf16 planes of the h tile: row r0 + 16 k, hidden 4 c4 .. 4 c4 + 3
 #pragma unroll
-    for (int k = 0; k < QH; ++k) {
-      float* dst = hl + l0 + k * RSTEP * SH;
-      dst[0] = buf[k].x;
-      dst[1] = buf[k].y;
-      dst[2] = buf[k].z;
-      dst[3] = buf[k].w;
+      for (int k = 0; k < QH; ++k) {
+        uint32_t p1[2], p2[2], p3[2];
+        split3_pk(buf[k].x, buf[k].y, p1[0], p2[0], p3[0]);
+        split3_pk(buf[k].z, buf[k].w, p1[1], p2[1], p3[1]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(hl) + (r0 + k * RSTEP) * 8 + 2 * c4;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(p1[0], p1[1]);
+        *reinterpret_cast<uint2*>(dst + kSbPlane) = make_uint2(p2[0], p2[1]);
+        *reinterpret_cast<uint2*>(dst + 2 * kSbPlane) = make_uint2(p3[0], p3[1]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < QH; ++k) {
+        float* dst = hl + l0 + k * RSTEP * SH;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
     }
     const float z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
     wave_lds_sync();
     issue(tile + ustep);
     flush();
+    if constexpr (SB) {
+      // A fragments [h3 | h2], [h1 | h1], [h2 | h1]: plane (ak < 2 ? 2 : 1), 0, (ak < 2 ? 1 : 0)
+      const uint32_t* pl = reinterpret_cast<const uint32_t*>(hl) + 4 * (ak & 1);
+      const int pa = ak < 2 ? 2 * kSbPlane : kSbPlane, pc = ak < 2 ? kSbPlane : 0;
+      f32x4v acc[NN][4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {  // one M tile's fragments live at a time
+        const uint32_t* row = pl + (16 * mt + am) * 8;
+        const bf16x8v h0 = frag8(*reinterpret_cast<const u32x4v*>(row + pa));
+        const bf16x8v h1 = frag8(*reinterpret_cast<const u32x4v*>(row));
+        const bf16x8v h2 = frag8(*reinterpret_cast<const u32x4v*>(row + pc));
+#pragma unroll
+        for (int nt = 0; nt < NN; ++nt) {
+          acc[nt][mt] = mfma_bf16(h0, wsb[nt][0], f32x4v{0.0f, 0.0f, 0.0f, 0.0f});
+          acc[nt][mt] = mfma_bf16(h1, wsb[nt][1], acc[nt][mt]);
+          acc[nt][mt] = mfma_bf16(h2, wsb[nt][2], acc[nt][mt]);
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt) {  // every plane read is done: t overlays the planes
+        const int n = 16 * nt + am;
+        if (n < P) {
+          const float bn = da.bias ? da.bias[n] : 0.0f;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            *reinterpret_cast<f32x4v*>(tl + n * kCS + 16 * mt + 4 * ak) = acc[nt][mt] + bn;
+        }
+      }
+    } else {
     // t = h W + b on the matrix cores, 16 columns at a time (exact fp32); the A
     // fragments (4 M tiles x QH k-steps) are shared by every N tile
     float av[4][QH];
@@ -264,6 +340,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
         for (int mt = 0; mt < 4; ++mt)
           *reinterpret_cast<f32x4v*>(tl + n * kCS + 16 * mt + 4 * ak) = acc[mt] + bn;
       }
+    }
     }
     wave_lds_sync();
     const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM, false>(z0, tl + lane, a)
@@ -791,13 +868,21 @@ bool launch_pd_dm(int dm, const DenseArgs& da, hipStream_t s, int64_t* g) {
 
 #endif  // NFN_DENSE_HP
 
+// the split-bf16 t GEMM for H = 16, P <= 32 (release default; diag NFN_DENSE_SB=0: fp32 MFMA)
+constexpr int kDenseSplitBf16 = 1;
 template <int QH, int CM>
 void launch_d1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
-  const size_t lds = (size_t)(4 * QH * nn * 16 + 4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
+  bool sb = false;
+  if constexpr (QH == 4) sb = nn <= 2 && env_int("NFN_DENSE_SB", kDenseSplitBf16) != 0;
+  const int wf = sb ? dense1_sb_wave_floats(da.c.P, da.h_lds_stride) : dense1_wave_floats(da.c.P, da.h_lds_stride);
+  const size_t lds = (size_t)(4 * QH * nn * 16 + 4 * wf + 16) * sizeof(float);
   auto kfn = nn <= 1 ? chain_dense1_kernel<QH, 1, CM>
                      : (nn == 2 ? chain_dense1_kernel<QH, 2, CM> : (nn == 3 ? chain_dense1_kernel<QH, 3, CM>
                                                                            : chain_dense1_kernel<QH, 4, CM>));
+  if constexpr (QH == 4) {
+    if (sb) kfn = nn <= 1 ? chain_dense1_kernel<QH, 1, CM, true> : chain_dense1_kernel<QH, 2, CM, true>;
+  }
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);

@@ -11,13 +11,11 @@
 // Persistent grid, every wave owns a stream of 64-sample tiles; per wave LDS: the h
 // tile (odd stride SH), the t / dt tile (odd stride S) and the flow inputs z_k.
 #include "nfn_grad_device.h"
+#include "nfn_bf16.h"
 #include "nfn_launch.h"
 
 namespace nfn {
 namespace {
-
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
 template <int DM, bool FAST, int MH, int NN>
 __global__ void __launch_bounds__(kMaxBlock) chain_dense_grad_kernel(DenseGradArgs g) {
@@ -488,7 +486,8 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
 }
 
 // ---------------------------------------------------------------------------------------
-// Split-bf16 weight-gradient GEMMs (diag NFN_DGRAD_SB): chain_dense1_grad_kernel (H = 16,
+// Split-bf16 weight-gradient GEMMs (the release form; diag NFN_DGRAD_SB=0 runs the f32
+// kernel): chain_dense1_grad_kernel (H = 16,
 // P <= 32) with dh^T = W dt^T and dW += h^T dt on v_mfma_f32_16x16x32_bf16 instead of
 // v_mfma_f32_16x16x4_f32 (t = h W stays f32: the chain amplifies t's rounding, and a
 // split-bf16 t — a few ulp, not bitwise numpy's / the forward kernel's — put one
@@ -515,31 +514,6 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_grad_kernel(DenseGradA
 //     ds_read_b128; A = W's parts, registers) and dW += h_i^T dt_j (B = the plane read
 //     transposed, ds_read_b64_tr_b16).
 // LDS per wave: the f32 kernel's (the plane needs 64 x 16 dwords).
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-typedef short s16x4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
-
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-  const bf16x2v v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32: round to nearest even
-  return __builtin_bit_cast(uint32_t, v);
-}
-__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-// (a, b) = (hi + mi + lo) exactly, each a packed bf16 pair (element 0 = a in the low half)
-__device__ __forceinline__ void split3_pk(float a, float b, uint32_t& hi, uint32_t& mi, uint32_t& lo) {
-  hi = pk_bf16(a, b);
-  const float ra = a - bf16_lo(hi), rb = b - bf16_hi(hi);
-  mi = pk_bf16(ra, rb);
-  lo = pk_bf16(ra - bf16_lo(mi), rb - bf16_hi(mi));
-}
-__device__ __forceinline__ bf16x8v frag8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const u32x4v v = {a, b, c, d};
-  return __builtin_bit_cast(bf16x8v, v);
-}
-__device__ __forceinline__ f32x4v mfma_bf16(bf16x8v a, bf16x8v b, f32x4v c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 // two transposed 4 x 16 reads (ds_read_b64_tr_b16 at two LDS addresses) as one fragment
 __device__ __forceinline__ bf16x8v tr_frag(const float* base0, const float* base1) {
   const s16x4v x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(

@@ -43,7 +43,9 @@ def _case(ft, d, H, B, seed, bias=True):
                                       # pair bodies, hpair_types): (P, R) x 3 + P, (R, P) x 4 + R, P x 5
                                       (("planar", "radial") * 3 + ("planar",), 1, 16, 500),
                                       (("radial", "planar") * 4 + ("radial",), 1, 8, 300),
-                                      (("planar",) * 5, 1, 4, 257)])
+                                      (("planar",) * 5, 1, 4, 257),
+                                      # H = 16 with one sixteen-column N tile (P = 14): the split-bf16 t GEMM
+                                      (("radial", "planar") * 2, 1, 16, 300)])
 def test_dense_matches_oracle(math_mode, ft, d, H, B):
     from normalizingflownetwork_amd import ops
 
