@@ -524,7 +524,7 @@ __device__ __forceinline__ float planar1_uh(float u, float w, float rn, float m)
 // fp32 emulation of the C2 chain (tools/kernel_emu.py "r6" vs "r5", 2^20 random samples,
 // correctly rounded transcendentals): beyond 3e-6 relative 110 -> 31, beyond 1e-5 4 -> 1
 // (profiles/r06/r06_kernel_emu_m_forms.txt); on the GPU, every sample of C2 / C4 against the
-// fp64 oracle: beyond 1e-5 relative 36 / 317 -> 19 / 138 (profiles/r06/r06g_parity.json).
+// fp64 oracle: beyond 1e-5 relative 36 / 317 -> 19 / 138 (profiles/r06/r06h/r06h_parity.json).
 // The d = 1 fast-math forwards of log_prob, the posterior, the grid and the Bijector API form
 // m here (planar1_fast<true>, grid1_prepare), so their per-sample values stay bitwise one
 // another's.
@@ -543,8 +543,9 @@ __device__ __forceinline__ float planar1_m(float w, float u, float sp) {
 
 // ACCM: the cancellation-aware m (planar1_m) — every d = 1 fast-math forward except the
 // compute-bound fused Dense kernels and the backward (ACCM = false: m = softplus - (1 - 1e-5),
-// round 5's form; measured costs of the accurate m there, profiles/r06/r06g_*: fused Dense
-// forward +6 %, backward +1 %; C2 / C4 / C5 streams unchanged)
+// round 5's form; measured costs of the accurate m, profiles/r06/r06g/ and r06h/: fused Dense
+// forward +6 %, backward +1 %; C2 +0.3 %, C5 +1.7 %).  Not adopted on top (r06o): a Newton step
+// on 1 / |w|^2 (C2 / C4 beyond 1e-5 19 / 138 -> 20 / 126 for C2 +1 %, C5 +5.6 %).
 template <bool ACCM = true>
 __device__ __forceinline__ float planar1_fast(float& z, float u, float wraw, float b) {
   const float w = wraw + 1.0f;

@@ -460,5 +460,42 @@ FORMS["r6+tx"] = (make_planar_mdelta_r(0.75, 7, tanh=tanh_exact), radial_r3, bas
 FORMS["md2.0+tx"] = (make_planar_mdelta_r(2.0, 13, tanh=tanh_exact), radial_r3, base_r3)
 
 
+def make_planar_r6x(tanh=tanh_t3, rn_newton=False, uh_div=False):
+    """Round 6's shipped planar form (planar1_m, |d| <= 0.75) with the attribution's next
+    candidates: a Newton-refined 1 / (w^2 + 1e-9) (two fma) and a corrected u_hat quotient."""
+    cf, RR = fit_m_poly(0.75, 7), F(0.75)
+
+    def planar(z, u, wraw, b):
+        w = wraw + F(1)
+        wtu = w * u
+        nw2 = fma(w, w, F(1e-9))
+        rn = rcp(nw2)
+        if rn_newton:
+            rn = fma(fma(-nw2, rn, F(1)), rn, rn)
+        sp = softplus_alpha(wtu)
+        d = fma(w, u, -X0H) - X0L
+        p = cf[-1]
+        for c in cf[-2::-1]:
+            p = fma(d, p, c)
+        m = np.where(np.abs(d) <= RR, fma(d, p, F(1e-5)), sp - ONE_M)
+        num = fma(u, F(1e-9), m * w)
+        uh = num * rn
+        if uh_div:
+            uh = fma(fma(-nw2, uh, num), rn, uh)
+        qd = fma((wtu - m) * F(1e-9), rn, sp + F(1e-5))
+        th = tanh(fma(w, z, b))
+        z = fma(uh, th, z)
+        return z, fma(th, th, fma(-th, th, F(1)) * qd)
+    return planar
+
+
+FORMS["r6+rn"] = (make_planar_r6x(rn_newton=True), radial_r3, base_r3)
+FORMS["r6+ud"] = (make_planar_r6x(uh_div=True), radial_r3, base_r3)
+FORMS["r6+rn+ud"] = (make_planar_r6x(rn_newton=True, uh_div=True), radial_r3, base_r3)
+FORMS["r6+tacc"] = (make_planar_r6x(tanh=tanh_acc), radial_r3, base_r3)
+FORMS["r6+tx+ud"] = (make_planar_r6x(tanh=tanh_exact, uh_div=True), radial_r3, base_r3)
+FORMS["r6+tacc+ud"] = (make_planar_r6x(tanh=tanh_acc, uh_div=True), radial_r3, base_r3)
+
+
 if __name__ == "__main__":
     main()
