@@ -538,12 +538,18 @@ __host__ __device__ inline int dense1_grad_sb_wave_floats(int P, int K) {
 }
 constexpr int kSbWRow = 16;  // dwords per hidden unit of the W parts (16 pairs of p, chunks swizzled as the planes)
 constexpr int kSbWFloats = 3 * 16 * kSbWRow + 32;  // the workgroup's W bf16 parts [part][hidden][pairs of p] and bias
+// The programs the fused Dense backward runs as compile-time blocks with the parameter-scalar
+// cache (SP indexes them): C2's (planar, radial) x 5, and the estimator's default
+// NormalizingFlowNetwork(n_dims, n_flows=10), radial x 10 (NormalizingFlowNetwork.py:10-17).
+constexpr uint32_t kCacheTypes[] = {0x44444u, 0x55555u};
+constexpr int kCacheK[] = {10, 10};
+constexpr int kNumCached = 2;
 
 // CM: the chain form.  The compile-time C2 program (diag kStaticProg, grad1_static) and its
 // parameter-scalar cache (kStaticCache, grad1_static_cache: the release form for C2's program;
 // diag kStaticCacheX, the cache bitwise grad1_static's) run at 2 waves per SIMD (the static
 // form spills at 3), every other form at 3.
-template <int NN, int CM = kChainPairs>
+template <int NN, int CM = kChainPairs, int SP = 0>
 __global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStaticCacheX || CM == kStaticProg) ? 2 : 3)
     chain_dense1_grad_sb_kernel(DenseGradArgs g) {
   static_assert(NN == 1 || NN == 2, "P <= 32");
@@ -684,7 +690,7 @@ __global__ void __launch_bounds__(kMaxBlock, (CM == kStaticCache || CM == kStati
     float adj, z = z0;
     float lp;
     if constexpr (CM == kStaticCache || CM == kStaticCacheX)
-      lp = grad1_static_cache<kStaticTypes[0], kStaticK[0], kCS, CM == kStaticCache>(z, tl + lane, P, trainable, gl,
+      lp = grad1_static_cache<kCacheTypes[SP], kCacheK[SP], kCS, CM == kStaticCache>(z, tl + lane, P, trainable, gl,
                                                                                       a.out != nullptr, adj) - corr;
     else if constexpr (CM == kStaticProg)
       lp = grad1_static<kStaticTypes[0], kStaticK[0], kCS>(z, tl + lane, zh, 64, P, trainable, gl, a.out != nullptr,
@@ -873,20 +879,24 @@ constexpr int kDgradSplitBf16 = 1;
 template <int NN>
 int64_t launch_dg1_sb(const DenseGradArgs& g, int64_t max_parts, hipStream_t s) {
   auto kfn = chain_dense1_grad_sb_kernel<NN, kChainPairs>;
-  // C2's program, (planar, radial) x 5, at compile time with the parameter-scalar cache: 0.977 vs
+  // a cached program (kCacheTypes) at compile time with the parameter-scalar cache: C2's 0.950 vs
   // 1.066 ms without the cache and 1.158 for the runtime program's pair form in one bench-harness
-  // A/B (profiles/r06/r06i_*); the diag build's NFN_CHAIN_FORM picks the others
-  const bool c2prog = NN == 2 && g.da.c.prog.K == kStaticK[0] && g.da.c.prog.types[0] == kStaticTypes[0];
+  // A/B (profiles/r06/r06k/); the diag build's NFN_CHAIN_FORM picks the others
+  int sp = -1;
+  for (int i = 0; i < kNumCached; ++i)
+    if (g.da.c.prog.K == kCacheK[i] && g.da.c.prog.types[0] == kCacheTypes[i]) sp = i;
   if constexpr (NN == 2) {
-    if (c2prog) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCache>;
+    if (sp == 0) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCache, 0>;
+    if (sp == 1) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCache, 1>;
   }
 #ifdef NFN_DIAG
   const int cf = env_int("NFN_CHAIN_FORM", -1);
   if (cf == kChainLoop) kfn = chain_dense1_grad_sb_kernel<NN, kChainLoop>;
   if (cf == kChainPairs) kfn = chain_dense1_grad_sb_kernel<NN, kChainPairs>;
   if constexpr (NN == 2) {
-    if (c2prog && cf == kStaticProg) kfn = chain_dense1_grad_sb_kernel<NN, kStaticProg>;
-    if (c2prog && cf == kStaticCacheX) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCacheX>;
+    if (sp == 0 && cf == kStaticProg) kfn = chain_dense1_grad_sb_kernel<NN, kStaticProg>;
+    if (sp == 0 && cf == kStaticCacheX) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCacheX, 0>;
+    if (sp == 1 && cf == kStaticCacheX) kfn = chain_dense1_grad_sb_kernel<NN, kStaticCacheX, 1>;
   }
 #endif
   const size_t lds = ((size_t)4 * dense1_grad_sb_wave_floats(g.da.c.P, g.da.c.prog.K) + kSbWFloats) * sizeof(float);

@@ -250,6 +250,24 @@ def dense_cache():
             rel[what] = {"max": float(r.max()), "p999": float(torch.quantile(r[:1 << 20], 0.999)),
                          "n_beyond_1e-5": int((r > 1e-5).sum()), "n": int(r.numel())}
         res[f"B{B}"] = {"exact_cache": "bitwise", "shared_vs_static": rel}
+        # the estimator's default program, radial x 10 (no planar flow: the release form is the
+        # exact cache), against the runtime program's pair form
+        W10 = torch.randn((16, 32), generator=gen, device="cuda") / 4.0
+        outs = {}
+        for cm in ("3", "4", "5"):
+            os.environ["NFN_CHAIN_FORM"] = cm
+            try:
+                outs[cm] = ops.chain_log_prob_dense_grad(y, h, W10, b, ("radial",) * 10, 1, True, g_out=g,
+                                                         want_logp=True)
+            finally:
+                os.environ.pop("NFN_CHAIN_FORM")
+        for x4, x5, what in zip(outs["4"], outs["5"], names):
+            same = (x4 == x5) | (torch.isnan(x4) & torch.isnan(x5))
+            assert bool(same.all()), f"radial x 10 B={B} {what}: {int((~same).sum())} values differ (release vs exact)"
+        lp3, lp4 = outs["3"][0], outs["4"][0]
+        ok = torch.isfinite(lp3) & (lp3.abs() < 1e4)
+        assert torch.allclose(lp4[ok], lp3[ok], rtol=1e-5, atol=1e-5), f"radial x 10 B={B}: cache vs pairs log_prob"
+        res[f"R10_B{B}"] = "bitwise"
     return res
 
 

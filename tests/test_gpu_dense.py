@@ -175,6 +175,8 @@ def test_posterior_dense_full_size_c5_sampled(gpu):
 @pytest.mark.parametrize("ft,d,H,B", [(("planar", "radial") * 5, 1, 16, 1000), (("radial", "radial"), 1, 4, 333),
                                       (("affine", "planar", "radial"), 3, 8, 300), (("planar", "affine"), 8, 16, 129),
                                       (("radial",) * 14, 1, 32, 201),
+                                      # the estimator's default radial x 10 at H = 16: a cached compile-time program
+                                      (("radial",) * 10, 1, 16, 777),
                                       # odd alternating / homogeneous programs (hpair_types)
                                       (("planar", "radial") * 3 + ("planar",), 1, 16, 500),
                                       (("radial", "planar") * 2 + ("radial",), 1, 8, 300),

@@ -86,3 +86,4 @@ def test_diag_dense_grad_scalar_cache_bitwise(gpu):
     print(res)
     assert res["library"] == "libnfn_hip_diag.so"
     assert sum(isinstance(v, dict) and v["exact_cache"] == "bitwise" for v in res.values()) == 2
+    assert sum(v == "bitwise" for k, v in res.items() if k.startswith("R10_")) == 2
