@@ -726,11 +726,15 @@ def main():
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
-            # fused Dense modes: the fp32 MFMA work per launch (t = hW, and for the backward
-            # dh = dt W^T, dW = h^T dt) against the 157.3 TF/s fp32 matrix peak
+            # fused Dense modes: the fp32 GEMM work per launch (t = hW, and for the backward
+            # dh = dt W^T, dW = h^T dt) in algorithmic fp32 FLOPs against the 157.3 TF/s fp32
+            # matrix peak; at H = 16, P <= 32 (d = 1, fast math) the kernels run t (forward) and
+            # dh, dW (backward) as exact 3-way split-bf16 products on v_mfma_f32_16x16x32_bf16
             "mfma": None if not dense_mode else {
                 "tflops": (3 if grad_mode else 1) * 2.0 * B * H * P * (1 if S is None else S) / (kern_ms * 1e-3) / 1e12,
-                "peak": 157.3},
+                "peak": 157.3,
+                "gemm_form": ("split-bf16 (t f32 MFMA in the backward)" if grad_mode else "split-bf16 t")
+                if (H == 16 and P <= 32 and d == 1 and S is None and args.math == "fast") else "f32 MFMA"},
             "mean_log_prob": mean_ll,
             "nonfinite_log_prob": nonfinite,
             "unfused_ms": unfused_ms,

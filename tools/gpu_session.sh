@@ -76,6 +76,13 @@ for s in $STEPS; do
         python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
       { cd /tmp; run pmc_write_grad 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_grad" -o w -- \
         python3 "$ROOT/bench.py" --mode grad --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; } ;;
+    pmc_dense)  # HBM traffic of the fused Dense forward and backward (separate FETCH / WRITE passes)
+      for m in dense dense_grad; do
+        { cd /tmp; run pmc_fetch_$m 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_$m" -o f -- \
+          python3 "$ROOT/bench.py" --mode $m --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+        { cd /tmp; run pmc_write_$m 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_$m" -o w -- \
+          python3 "$ROOT/bench.py" --mode $m --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT"; }
+      done ;;
     finish) run finish 300 python tools/microbench.py finish ;;
     c5micro) run c5micro 300 python tools/microbench.py c5 ;;
     micro) run micro 600 python tools/microbench.py C2 C3 C5 C1 ;;
