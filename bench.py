@@ -648,7 +648,9 @@ def main():
             metric = f"log_prob backward evals/sec (whole node), {args.config}"
         elif args.mode == "dense_grad":
             # dispatch-recorded events time the step's first launch; markers bracket both
-            kernel_name = ("chain_dense1_grad_kernel" if d == 1 and H in (16, 32) else "chain_dense_grad_kernel") + \
+            kernel_name = ("chain_dense1_grad_sb_kernel" if d == 1 and H == 16 and P <= 32 and args.math == "fast"
+                           else "chain_dense1_grad_kernel" if d == 1 and H in (16, 32) and args.math == "fast"
+                           else "chain_dense_grad_kernel") + \
                 ("" if ev_dispatch else " + sum_partials_kernel")
             metric = f"Dense(H={H})->log_prob backward evals/sec (whole node), {args.config}"
         elif args.mode == "bijector":
