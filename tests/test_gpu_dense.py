@@ -61,6 +61,29 @@ def test_dense_matches_oracle(math_mode, ft, d, H, B):
     assert abs(s.item() - ref64.sum()) <= bound.sum() + 1e-6 * abs(ref64.sum())
 
 
+@pytest.mark.parametrize("B,bias,hs", [(37, False, 16), (64 * 9 + 1, True, 20), (4096, False, 24)])
+def test_dense_split_t_views_and_tails(gpu, B, bias, hs):
+    """The split-bf16 t GEMM (H = 16, P <= 32: chain_dense1_kernel SB) on h row views of a wider
+    buffer, with and without bias, on batches that end inside a tile (and one shorter than a
+    tile), against the oracle on t = h W + b."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d, H = ("planar", "radial") * 5, 1, 16
+    h, W, b, y, t64, t32 = _case(ft, d, H, B, seed=B + hs, bias=bias)
+    hbuf = np.zeros((B, hs), np.float32)
+    hbuf[:, :H] = h
+    hv = torch.from_numpy(hbuf).cuda()[:, :H]
+    bb = None if b is None else torch.from_numpy(b).cuda()
+    out, s = ops.chain_log_prob_dense(torch.from_numpy(y).cuda(), hv, torch.from_numpy(W).cuda(), bb, ft, d, True,
+                                      want_sum=True)
+    ref64 = O.chain_log_prob(y, t64, ft, d, True, np.float64)
+    ref32 = O.chain_log_prob(y, t32, ft, d, True, np.float32)
+    check_forward(out.cpu().numpy(), ref64, ref32, f"dense split-t views B={B} row stride {hs} bias={bias}",
+                  kind="dense", sensitivity=fp32_sensitivity(y, t32, ft, d, True))
+    bound = O.tolerance_bound(ref64, ref32)
+    assert abs(s.item() - ref64.sum()) <= bound.sum() + 1e-6 * abs(ref64.sum())
+
+
 def test_dense_with_normalisation_and_fallback(gpu):
     """With and without bias, with the fused y normalisation, and through the
     unsupported-shape fallback (H = 10: library GEMM + chain kernel), against the
@@ -399,7 +422,10 @@ def test_dense_grad_fallback_matches_unfused(gpu):
     (("affine", "planar", "radial", "affine"), 16, 640, False, True),
     (("radial", "planar") * 3 + ("affine",), 32, 64 * 9 + 63, True, True),
     (("planar",) * 16, 32, 77, False, False),
-    (("radial",), 16, 1, True, False)])
+    (("radial",), 16, 1, True, False),
+    # the cached compile-time programs (C2's with a fixed base, the estimator's radial x 10)
+    (("planar", "radial") * 5, 16, 200, False, True),
+    (("radial",) * 10, 16, 64 * 5 + 17, True, True)])
 def test_dense1_grad_kernel_shapes(gpu, ft, H, B, trainable, g_none):
     """The d = 1 fast-math fused Dense backward (chain_dense1_grad_kernel: H in {16, 32},
     P <= 64) over ragged batches, widths P not a multiple of 16, a fixed base, a missing
