@@ -190,7 +190,11 @@ int32_t nfn_chain_logprob_grad_f32(const float* y, int64_t y_bstride, const floa
 
 /*
  * Output Dense layer fused into the chain: t_b = h_b W + bias (never written to
- * memory), then exactly nfn_chain_logprob_f32 on t.
+ * memory), then the chain as nfn_chain_logprob_f32 evaluates it.  Numerics: at d = 1
+ * (fast math) the chain keeps round 5's m = softplus(w u) - 1 + 1e-5 (the compute-bound
+ * fused kernels do not take the cancellation-aware form), and at H = 16, P <= 32 t is formed
+ * from exact 3-way bf16 splits of h and W on the bf16 matrix cores (six products per fp32
+ * product, fp32 accumulation): fp32-level, not bitwise an fp32 GEMM.
  *   h    : (B, H) rows at h_rowstride floats (>= H, multiple of 4), 16-byte aligned;
  *          H in {4, 8, 16, 32, 64}
  *   W    : (H, P) row-major, P = nfn_total_param_size <= 64;  bias : (P,) or NULL
@@ -314,7 +318,8 @@ int32_t nfn_posterior_lse_f32(const float* y, int64_t y_bstride, const float* t,
  *   grad_y : (B, d) contiguous (nullable);  out_logp : (B,) (nullable)
  *   workspace : device float[nfn_dense_grad_workspace_floats(B, H, P)] (needed with grad_W / grad_b)
  * Shapes as nfn_chain_logprob_dense_f32 (H in {4..64}, P <= 64, d <= 8), and the tile's
- * flow inputs must fit LDS; other shapes return NFN_E_SHAPE.
+ * flow inputs must fit LDS; other shapes return NFN_E_SHAPE.  At d = 1, H = 16, P <= 32
+ * (fast math) t stays an fp32 MFMA GEMM while dh and dW use exact 3-way bf16 splits.
  */
 int64_t nfn_dense_grad_workspace_floats(int64_t B, int32_t H, int32_t P);
 int32_t nfn_chain_logprob_dense_grad_f32(const float* y, int64_t y_bstride, const float* h, int64_t h_rowstride,
