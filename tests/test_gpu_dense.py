@@ -168,6 +168,33 @@ def test_posterior_dense_normalised_nobias_and_fallback(gpu):
         check_forward(out.cpu().numpy(), ref64, ref32, f"posterior dense normalised H={H} bias={bias}", kind="dense")
 
 
+def test_dense_full_size_c2_sampled(gpu):
+    """The fused Dense forward at the C2 batch (2^24 rows, H = 16: the split-bf16 t GEMM) on
+    y / h with the bench's scale: 65,536 random rows against the oracle on t = h W + b (the
+    fp32 sensitivity widening as everywhere), every value finite, and the fused fp64 sum equal
+    to the sum of the returned values."""
+    from normalizingflownetwork_amd import ops
+
+    ft, d, B, H = ("planar", "radial") * 5, 1, 1 << 24, 16
+    P = O.total_param_size(ft, d, True)
+    gen = torch.Generator(device="cuda").manual_seed(24)
+    h = torch.randn((B, H), generator=gen, device="cuda")
+    W = torch.randn((H, P), generator=gen, device="cuda") / 4.0
+    b = 0.1 * torch.randn((P,), generator=gen, device="cuda")
+    y = torch.randn((B, d), generator=gen, device="cuda")
+    out, s = ops.chain_log_prob_dense(y, h, W, b, ft, d, True, want_sum=True)
+    assert torch.isfinite(out).all()
+    idx = torch.randperm(B, generator=torch.Generator().manual_seed(3))[:1 << 16].cuda()
+    hs, Wn, bn, ys = h[idx].cpu().numpy(), W.cpu().numpy(), b.cpu().numpy(), y[idx].cpu().numpy()
+    t64 = hs.astype(np.float64) @ Wn.astype(np.float64) + bn.astype(np.float64)
+    t32 = (hs @ Wn + bn).astype(np.float32)
+    ref64 = O.chain_log_prob(ys, t64, ft, d, True, np.float64)
+    ref32 = O.chain_log_prob(ys, t32, ft, d, True, np.float32)
+    check_forward(out[idx].cpu().numpy(), ref64, ref32, "dense C2 full batch (65536 random rows)", kind="dense",
+                  sensitivity=fp32_sensitivity(ys, t32, ft, d, True))
+    assert abs(s.item() - out.double().sum().item()) <= 1e-9 * abs(s.item()) + 1e-6
+
+
 def test_posterior_dense_full_size_c5_sampled(gpu):
     """C5 per-GPU shape (S = 64 draws x B = 2^17, H = 16): the fused kernel equals the
     unfused path (t_s materialised by the library GEMM, then the posterior kernel)
