@@ -359,6 +359,9 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
   }
 }
 
+// (Measured and removed: the split-bf16 t_s of chain_dense1_kernel<SB> here, W_s split per unit
+// in registers and h_s into LDS planes, ran C5 at 0.2285 vs 0.2186 ms — W_s changes every
+// unit, so the splits cost more than the MFMAs save; commit 5510a5c, profiles/r06/r06u/.)
 // Bayesian posterior with the output DenseVariational layer fused
 // (BayesianNNEstimator.py:65-76 score over draws, :136-145 the variational output
 // layer): per sample, logsumexp over S draws of log_prob(y | t_s = h_s W_s + b_s) - log S.
@@ -367,10 +370,7 @@ __global__ void __launch_bounds__(kMaxBlock) chain_dense1_kernel(DenseArgs da) {
 // W / bias fragments are prefetched (buffer loads, counted waits) while the current
 // unit runs the MFMA GEMM and the chain; the tile's result leaves once, after its
 // last draw (the per-unit store of the other draws goes through an empty descriptor).
-// SB (H = 16, P <= 32): t_s = h_s W_s on v_mfma_f32_16x16x32_bf16 as in chain_dense1_kernel<SB>;
-// W_s changes every unit, so each unit splits both operands (h at the hand-off into LDS
-// planes, W_s's fragments in registers).
-template <int QH, int NN, int CM = kChainLoop, bool SB = false>
+template <int QH, int NN, int CM = kChainLoop>
 __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs da) {
   const ChainArgs& a = da.c;
   extern __shared__ float lds[];
@@ -383,8 +383,7 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
   const int SH = da.h_lds_stride;
   const int P = a.P;
   const int S = a.S;
-  static_assert(!SB || (QH == 4 && NN <= 2), "split-bf16 t: H = 16, P <= 32");
-  float* hl = lds + wid * (SB ? dense1_sb_wave_floats(P, SH) : dense1_wave_floats(P, SH));
+  float* hl = lds + wid * dense1_wave_floats(P, SH);
   float* tl = hl;
   const int r0 = lane / QH, c4 = lane % QH;
   const int l0 = r0 * SH + 4 * c4;
@@ -411,19 +410,9 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
 #pragma unroll
     for (int ks = 0; ks < QH; ++ks) woff[ks][nt] = wcol[nt] ? ((4 * ks + ak) * P + 16 * nt + am) * 4 : 0;
   }
-  // SB: this lane's W_s column 16 nt + am at hidden 8 (ak & 1) + j, j < 8 (byte offsets)
-  constexpr int NJ = SB ? 8 : 1;
-  int wsoff[SB ? NN : 1][NJ];
-  if constexpr (SB) {
-#pragma unroll
-    for (int nt = 0; nt < NN; ++nt)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) wsoff[nt][jj] = wcol[nt] ? ((8 * (ak & 1) + jj) * P + 16 * nt + am) * 4 : 0;
-  }
   float4 buf[QH];
   float ybuf;
-  float wbuf[SB ? 1 : QH][SB ? 1 : NN], bbuf[NN];
-  float wsb_raw[SB ? NN : 1][NJ];
+  float wbuf[QH][NN], bbuf[NN];
   auto issue = [&](int64_t tile, int sd) {
     const int64_t b0 = tile * 64;
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
@@ -435,19 +424,11 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
     for (int k = 0; k < QH; ++k)
       buf[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, hoff, k * kstep, kNT));
     const auto rw = tile_rsrc(da.W + sd * da.w_drawstride, nr > 0 ? (int64_t)4 * QH * P * 4 : 0);
-    if constexpr (SB) {
+#pragma unroll
+    for (int ks = 0; ks < QH; ++ks)
 #pragma unroll
       for (int nt = 0; nt < NN; ++nt)
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj)
-          wsb_raw[nt][jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, wsoff[nt][jj], 0, 0));
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < QH; ++ks)
-#pragma unroll
-        for (int nt = 0; nt < NN; ++nt)
-          wbuf[ks][nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, woff[ks][nt], 0, 0));
-    }
+        wbuf[ks][nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, woff[ks][nt], 0, 0));
     const auto rb = tile_rsrc(da.bias ? da.bias + sd * da.b_drawstride : da.W, (da.bias && nr > 0) ? P * 4 : 0);
 #pragma unroll
     for (int nt = 0; nt < NN; ++nt)
@@ -467,48 +448,20 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
     const int64_t nr = max((int64_t)0, min((int64_t)64, a.B - b0));
     float m = -INFINITY, lacc = 0.0f;
     for (int sd = 0; sd < S; ++sd) {
-      float wv[SB ? 1 : QH][SB ? 1 : NN], bv[NN];
-      bf16x8v wsb[SB ? NN : 1][3];
-      if constexpr (SB) {  // h_s's three bf16 planes; W_s's B fragments [W1 ; W2], [W3 ; W2], [W1 ; W1]
 #pragma unroll
-        for (int k = 0; k < QH; ++k) {
-          uint32_t p1[2], p2[2], p3[2];
-          split3_pk(buf[k].x, buf[k].y, p1[0], p2[0], p3[0]);
-          split3_pk(buf[k].z, buf[k].w, p1[1], p2[1], p3[1]);
-          uint32_t* dst = reinterpret_cast<uint32_t*>(hl) + (r0 + k * RSTEP) * 8 + 2 * c4;
-          *reinterpret_cast<uint2*>(dst) = make_uint2(p1[0], p1[1]);
-          *reinterpret_cast<uint2*>(dst + kSbPlane) = make_uint2(p2[0], p2[1]);
-          *reinterpret_cast<uint2*>(dst + 2 * kSbPlane) = make_uint2(p3[0], p3[1]);
-        }
+      for (int k = 0; k < QH; ++k) {
+        float* dst = hl + l0 + k * RSTEP * SH;
+        dst[0] = buf[k].x;
+        dst[1] = buf[k].y;
+        dst[2] = buf[k].z;
+        dst[3] = buf[k].w;
+      }
+      float wv[QH][NN], bv[NN];
 #pragma unroll
-        for (int nt = 0; nt < NN; ++nt) {
-          bv[nt] = bbuf[nt];
-          uint32_t w1[4], w2[4], w3[4];
+      for (int nt = 0; nt < NN; ++nt) {
+        bv[nt] = bbuf[nt];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float x0 = wcol[nt] ? wsb_raw[nt][2 * q] : 0.0f, x1 = wcol[nt] ? wsb_raw[nt][2 * q + 1] : 0.0f;
-            split3_pk(x0, x1, w1[q], w2[q], w3[q]);
-          }
-          const bool lo = ak < 2;
-          wsb[nt][0] = lo ? frag8(w1[0], w1[1], w1[2], w1[3]) : frag8(w2[0], w2[1], w2[2], w2[3]);
-          wsb[nt][1] = lo ? frag8(w3[0], w3[1], w3[2], w3[3]) : frag8(w2[0], w2[1], w2[2], w2[3]);
-          wsb[nt][2] = frag8(w1[0], w1[1], w1[2], w1[3]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < QH; ++k) {
-          float* dst = hl + l0 + k * RSTEP * SH;
-          dst[0] = buf[k].x;
-          dst[1] = buf[k].y;
-          dst[2] = buf[k].z;
-          dst[3] = buf[k].w;
-        }
-#pragma unroll
-        for (int nt = 0; nt < NN; ++nt) {
-          bv[nt] = bbuf[nt];
-#pragma unroll
-          for (int ks = 0; ks < QH; ++ks) wv[ks][nt] = wcol[nt] ? wbuf[ks][nt] : 0.0f;
-        }
+        for (int ks = 0; ks < QH; ++ks) wv[ks][nt] = wcol[nt] ? wbuf[ks][nt] : 0.0f;
       }
       const float z0 = norm ? f_div<true>(ybuf - ymean, ystd) : ybuf;
       wave_lds_sync();
@@ -516,33 +469,6 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
       issue(last ? tile + ustep : tile, last ? 0 : sd + 1);
       flush();
       pend_r = tile_rsrc(a.out, 0);  // later draws of this tile store nothing
-      if constexpr (SB) {
-        const uint32_t* pl = reinterpret_cast<const uint32_t*>(hl) + 4 * (ak & 1);
-        const int pa = ak < 2 ? 2 * kSbPlane : kSbPlane, pc = ak < 2 ? kSbPlane : 0;
-        f32x4v acc[NN][4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const uint32_t* row = pl + (16 * mt + am) * 8;
-          const bf16x8v h0 = frag8(*reinterpret_cast<const u32x4v*>(row + pa));
-          const bf16x8v h1 = frag8(*reinterpret_cast<const u32x4v*>(row));
-          const bf16x8v h2 = frag8(*reinterpret_cast<const u32x4v*>(row + pc));
-#pragma unroll
-          for (int nt = 0; nt < NN; ++nt) {
-            acc[nt][mt] = mfma_bf16(h0, wsb[nt][0], f32x4v{0.0f, 0.0f, 0.0f, 0.0f});
-            acc[nt][mt] = mfma_bf16(h1, wsb[nt][1], acc[nt][mt]);
-            acc[nt][mt] = mfma_bf16(h2, wsb[nt][2], acc[nt][mt]);
-          }
-        }
-#pragma unroll
-        for (int nt = 0; nt < NN; ++nt) {  // every plane read is done: t overlays the planes
-          const int n = 16 * nt + am;
-          if (n < P) {
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-              *reinterpret_cast<f32x4v*>(tl + n * kCS + 16 * mt + 4 * ak) = acc[nt][mt] + bv[nt];
-          }
-        }
-      } else {
       float av[4][QH];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -563,7 +489,6 @@ __global__ void __launch_bounds__(kMaxBlock) posterior_dense1_kernel(DenseArgs d
           for (int mt = 0; mt < 4; ++mt)
             *reinterpret_cast<f32x4v*>(tl + n * kCS + 16 * mt + 4 * ak) = acc[mt] + bv[nt];
         }
-      }
       }
       wave_lds_sync();
       const float lp = (a.prog.K <= 16 ? eval_chain1_fast<true, kCS, CM, false>(z0, tl + lane, a)
@@ -872,23 +797,13 @@ bool launch_pdp_h(const DenseArgs& da, hipStream_t s, int64_t* g) {
   return false;
 }
 
-// the split-bf16 t GEMM for H = 16, P <= 32 (release default; diag NFN_DENSE_SB=0: fp32 MFMA)
-constexpr int kDenseSplitBf16 = 1;
-// the same for the posterior's t_s (posterior_dense1_kernel<SB>): 0 until measured
-constexpr int kPosteriorSplitBf16 = 0;
 template <int QH, int CM>
 void launch_pd1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
-  bool sb = false;  // the split-bf16 t_s GEMM: diag A/B only (NFN_DENSE_SB_POST=1)
-  if constexpr (QH == 4) sb = nn <= 2 && env_int("NFN_DENSE_SB_POST", kPosteriorSplitBf16) != 0;
-  const int wf = sb ? dense1_sb_wave_floats(da.c.P, da.h_lds_stride) : dense1_wave_floats(da.c.P, da.h_lds_stride);
-  const size_t lds = (size_t)(4 * wf + 16) * sizeof(float);
+  const size_t lds = (size_t)(4 * dense1_wave_floats(da.c.P, da.h_lds_stride) + 16) * sizeof(float);
   auto kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1, CM>
                      : (nn == 2 ? posterior_dense1_kernel<QH, 2, CM> : (nn == 3 ? posterior_dense1_kernel<QH, 3, CM>
                                                                                 : posterior_dense1_kernel<QH, 4, CM>));
-  if constexpr (QH == 4) {
-    if (sb) kfn = nn <= 1 ? posterior_dense1_kernel<QH, 1, CM, true> : posterior_dense1_kernel<QH, 2, CM, true>;
-  }
   int64_t grid = persistent_grid(kfn, kMaxBlock, lds, (da.c.ntiles + 3) / 4);
   *grid_out = std::max<int64_t>(1, grid);
   nfn_launch(kfn, dim3((unsigned)*grid_out), dim3(kMaxBlock), lds, s, da);
@@ -956,6 +871,8 @@ bool launch_pd_dm(int dm, const DenseArgs& da, hipStream_t s, int64_t* g) {
 
 #endif  // NFN_DENSE_HP
 
+// the split-bf16 t GEMM for H = 16, P <= 32 (release default; diag NFN_DENSE_SB=0: fp32 MFMA)
+constexpr int kDenseSplitBf16 = 1;
 template <int QH, int CM>
 void launch_d1_form(const DenseArgs& da, hipStream_t s, int64_t* grid_out) {
   const int nn = (da.c.P + 15) >> 4;
